@@ -1,0 +1,26 @@
+# Builds the MI355X (gfx950) engine library and the CPU oracle.  `python -c "import
+# __graft_entry__ as g; g.build()"` runs the same steps.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+CSRC := sdfs_amd/csrc
+LIB := sdfs_amd/libsdfs_cdc.so
+OBJS := build/cdc_kernels.o build/cdc_engine.o
+
+all: $(LIB) oracle
+
+build/%.o: $(CSRC)/%.hip $(CSRC)/cdc_internal.h include/sdfs_cdc.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

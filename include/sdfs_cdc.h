@@ -1,0 +1,161 @@
+/*
+ * sdfs_cdc.h — C-ABI of the MI355X-native variable-block CDC + fingerprint engine.
+ *
+ * This is the drop-in boundary behind SDFS's hash-engine plugin surface
+ * (org.opendedup.hashing.AbstractHashEngine, src/org/opendedup/hashing/AbstractHashEngine.java:24-39).
+ * A JNI shim binds a new Java class
+ * org.opendedup.hashing.HipVariableSha256HashEngine to these entry points; the Python package
+ * sdfs_amd binds them with ctypes.  Plain pointers and sizes only: no torch / HIP types in the
+ * signatures (HIP streams and device pointers travel as void* / uint8_t*).
+ *
+ * Errors: every entry point returns an int status (SDFS_CDC_OK = 0, negative on failure) and
+ * records a message readable with sdfs_cdc_last_error() (thread-local).  The JNI shim maps a
+ * non-zero status to java.io.IOException, which is what getChunks throws today
+ * (SparseDedupFile.java:578-580).  Engine creation failure corresponds to the factory's
+ * SDFSLogger.fatal + System.exit(5) (HashFunctionPool.java:116-119); the shim decides.
+ *
+ * Threading: one engine may be shared by all SDFS flush threads (SparseDedupFile.java:100 is a
+ * static singleton), so every call is re-entrant and thread-safe (calls are serialised per
+ * engine context; see DESIGN.md "Host edge").
+ */
+#ifndef SDFS_CDC_H
+#define SDFS_CDC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDFS_CDC_ABI_VERSION 1
+
+enum sdfs_cdc_status {
+    SDFS_CDC_OK = 0,
+    SDFS_CDC_EINVAL = -1,   /* bad argument / unsupported parameter combination */
+    SDFS_CDC_ECAP = -2,     /* caller's output capacity too small */
+    SDFS_CDC_EHIP = -3,     /* HIP runtime / kernel error */
+    SDFS_CDC_ENOMEM = -4,   /* device or pinned host allocation failed */
+    SDFS_CDC_ENODEV = -5,   /* no usable gfx950 device */
+};
+
+/* hash-type (Main.hashType, HashFunctionPool.java:36-43,102-121) */
+enum sdfs_cdc_hash_algo {
+    SDFS_CDC_SHA256 = 0,     /* VARIABLE_SHA256      -> 32-byte SHA-256 */
+    SDFS_CDC_SHA256_160 = 1, /* VARIABLE_SHA256_160  -> first 20 bytes of SHA-256 (VariableSha256HashEngine.java:60-65) */
+    SDFS_CDC_MD5 = 2,        /* VARIABLE_MD5         -> 16-byte MD5 (VariableMD5HashEngine.java:55-58) */
+};
+
+/* minimum-length comparison of the (absent) rabinwindow jar — SURVEY.md A.3 knob */
+enum sdfs_cdc_min_cmp { SDFS_CDC_MIN_GT = 0 /* n > min_len (default) */, SDFS_CDC_MIN_GE = 1 };
+
+/* Engine parameters = the numbers SDFS passes to EnhancedFingerFactory
+ * (VariableSha256HashEngine.java:50-52) plus the unpinned predicate knobs. */
+typedef struct sdfs_cdc_params {
+    uint64_t poly;          /* 10923124345206883 = 0x26CE86126EF863 (VariableSha256HashEngine.java:41) */
+    uint32_t window;        /* HashFunctionPool.bytesPerWindow = 48 (HashFunctionPool.java:51) */
+    uint32_t min_len;       /* HashFunctionPool.minLen = Main.MIN_CHUNK_LENGTH = 4095 (Main.java:189) */
+    uint32_t max_len;       /* HashFunctionPool.maxLen = 32768 (131072 backup) (Config.java:162-166) */
+    uint32_t chunk_length;  /* Main.CHUNK_LENGTH = 262144 (41943040 backup) (Config.java:158) */
+    uint64_t pred_mask;     /* boundary predicate (fp & pred_mask) == pred_value; default 0xFFF / 0 */
+    uint64_t pred_value;
+    uint32_t min_cmp;       /* enum sdfs_cdc_min_cmp */
+    uint32_t hash_algo;     /* enum sdfs_cdc_hash_algo */
+    int32_t device;         /* HIP device ordinal */
+    uint32_t flags;         /* reserved, 0 */
+    uint64_t max_batch_bytes; /* host-batch staging size (pinned); 0 = default 256 MiB */
+} sdfs_cdc_params;
+
+typedef struct sdfs_cdc_engine sdfs_cdc_engine;
+
+/* Per-buffer output slots on the DEVICE for sdfs_cdc_run_device (all device pointers).
+ * Buffer b's chunk i lives at slot b*cap + i, i < counts[b]; chunks are ascending, contiguous
+ * and cover [0, len_b) exactly (the List<Finger> contract, SparseDedupFile.java:535-564). */
+typedef struct sdfs_cdc_dev_out {
+    uint32_t* counts;   /* [nbuf] */
+    uint32_t* starts;   /* [nbuf*cap]  Finger.start */
+    uint32_t* lens;     /* [nbuf*cap]  Finger.len */
+    uint8_t* digests;   /* [nbuf*cap*32] Finger.hash (digest_len bytes used, rest zero) */
+    uint32_t cap;       /* slots per buffer, >= sdfs_cdc_slot_cap(engine, max buffer length) */
+    uint32_t reserved;
+    /* Optional dense fingerprint table (the record set that is RCCL all-gathered across GPUs):
+     * record r = {digest[32], u64 buffer_id, u32 start, u32 len} = 48 bytes, ordered by
+     * (buffer, chunk).  NULL to skip.  *total receives the record count (device u32). */
+    uint8_t* records;
+    uint64_t records_cap;
+    uint32_t* total;    /* [1] device; required */
+} sdfs_cdc_dev_out;
+
+#define SDFS_CDC_RECORD_BYTES 48
+
+/* ---- lifecycle ---- */
+int sdfs_cdc_abi_version(void);
+/* Fill p with the reference defaults; backup_volume != 0 selects the --backup-volume profile
+ * (VolumeConfigWriter.java:298-307: chunk-size 40960 KiB, max segment 128 KiB). */
+int sdfs_cdc_params_default(sdfs_cdc_params* p, int backup_volume);
+/* new VariableSha256HashEngine(...) / new VariableMD5HashEngine() (HashFunctionPool.java:102-121). */
+int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out);
+/* AbstractHashEngine.destroy() */
+int sdfs_cdc_destroy(sdfs_cdc_engine* e);
+const char* sdfs_cdc_last_error(void);
+
+/* ---- AbstractHashEngine accessors ---- */
+int sdfs_cdc_is_variable_length(const sdfs_cdc_engine* e);   /* isVariableLength(): 1 */
+int sdfs_cdc_get_max_len(const sdfs_cdc_engine* e);          /* getMaxLen(): Main.CHUNK_LENGTH (VariableSha256HashEngine.java:106-109) */
+int sdfs_cdc_get_min_len(const sdfs_cdc_engine* e);          /* getMinLen(): HashFunctionPool.minLen (:111-114) */
+int sdfs_cdc_set_seed(sdfs_cdc_engine* e, int seed);         /* setSeed(): no-op (:116-120) */
+int sdfs_cdc_digest_len(const sdfs_cdc_engine* e);           /* 32 / 20 / 16 */
+/* Output slots a buffer of buf_len bytes can need: ceil-bound on len/shortest-chunk + 2. */
+uint32_t sdfs_cdc_slot_cap(const sdfs_cdc_engine* e, uint64_t buf_len);
+
+/* ---- AbstractHashEngine.getHash(byte[]) (VariableSha256HashEngine.java:58-67) ----
+ * Host bytes in, digest_len bytes out (computed on the GPU). */
+int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest);
+
+/* ---- AbstractHashEngine.getChunks(byte[], uuid) (VariableSha256HashEngine.java:71-86) ----
+ * One host buffer (1..CHUNK_LENGTH bytes, fresh CDC state).  Writes *count chunks into
+ * starts/lens/digests (digest_len bytes each, densely packed), capacity cap entries. */
+int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, uint32_t* starts,
+                        uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count);
+
+/* Batched getChunks over nbuf independent host buffers at base+offs[b], lens[b] (each chunked
+ * from fresh state; SURVEY.md 0 "every call starts from a fresh state").  Per-buffer slots of
+ * cap entries (digests packed digest_len bytes per slot).  Pinned staging + H2D + kernels + D2H. */
+int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs,
+                              const uint32_t* lens, uint32_t nbuf, uint32_t* counts, uint32_t* starts,
+                              uint32_t* lens_out, uint8_t* digests, uint32_t cap);
+
+/* ---- device-resident path (bench / multi-GPU) ----
+ * d_data: device bytes, 64-byte aligned.  Uniform layout: nbuf buffers of uniform_len bytes
+ * (a multiple of 64) at b*uniform_len — the SDFS write-buffer case (every flushed buffer is
+ * CHUNK_LENGTH bytes, WritableCacheBuffer.java:115).  buffer_id_base is added to b in the
+ * record table.  stream: hipStream_t or NULL (= the engine's own stream).  Asynchronous:
+ * returns after enqueueing; d_offs/d_lens are ignored (pass NULL). */
+int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs,
+                        const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len,
+                        uint64_t buffer_id_base, const sdfs_cdc_dev_out* out, void* stream);
+/* Ragged layout: buffer b = d_data[d_offs[b] .. d_offs[b]+d_lens[b]) (device arrays), offsets
+ * multiples of 64, non-overlapping, all inside the first data_bytes bytes of d_data (the
+ * write-accelerator path hands getChunks arbitrary lengths, WritableCacheBuffer.java:641-643). */
+int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
+                               const uint64_t* d_offs, const uint32_t* d_lens, uint32_t nbuf,
+                               uint64_t buffer_id_base, const sdfs_cdc_dev_out* out, void* stream);
+/* Block until the engine's own stream has drained. */
+int sdfs_cdc_stream_sync(sdfs_cdc_engine* e);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around every kernel of the
+ * next runs (a ring of `nruns` event sets; 0 disables).  sdfs_cdc_kernel_times waits for the
+ * recorded events and returns, per pipeline stage, the average milliseconds over the last
+ * min(nruns, runs since set_timing) runs; returns the number of stages written. */
+int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns);
+int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int n);
+
+/* Synthetic input generator, device side: fills d_out[0..n) with byte
+ * (offset+i) of stream `stream` (counter-based SplitMix64; same bytes as the CPU definition). */
+int sdfs_cdc_synth_device(sdfs_cdc_engine* e, uint8_t* d_out, uint64_t n, uint64_t seed,
+                          uint64_t stream, uint64_t offset, void* stream_handle);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDFS_CDC_H */

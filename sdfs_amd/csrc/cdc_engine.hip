@@ -1,0 +1,624 @@
+// cdc_engine.hip — host side of the C-ABI (include/sdfs_cdc.h): engine lifecycle, device
+// workspace, the device-resident pipeline, and the host-buffer paths (getChunks / getHash /
+// batched getChunks) with pinned staging.  Drop-in for org.opendedup.hashing.AbstractHashEngine
+// (AbstractHashEngine.java:24-39) as implemented by VariableSha256HashEngine /
+// VariableMD5HashEngine (VariableSha256HashEngine.java:41-121, VariableMD5HashEngine.java:37-108).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/sdfs_cdc.h"
+#include "cdc_internal.h"
+
+using namespace sdfs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            return fail(SDFS_CDC_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),     \
+                        __FILE__, __LINE__);                                                      \
+    } while (0)
+
+int poly_degree(uint64_t p) { return p ? 63 - __builtin_clzll(p) : -1; }
+
+uint64_t mulx_mod(uint64_t v, uint64_t poly, int d) {
+    v <<= 1;
+    if ((v >> d) & 1) v ^= poly;
+    return v;
+}
+
+// Rolling-hash tables (same definition as the jar's precompute), laid out as the
+// scan kernel's LDS image with kTabCopies lane-private copies.
+std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window) {
+    const int d = poly_degree(poly);
+    std::vector<uint64_t> push(256), pop(256);
+    for (uint64_t i = 0; i < 256; i++) {
+        uint64_t r = i;  // i mod P (deg P > 8)
+        for (int k = 0; k < d; k++) r = mulx_mod(r, poly, d);
+        push[i] = (i << d) ^ r;
+        uint64_t q = i;
+        for (uint32_t k = 0; k < 8 * window; k++) q = mulx_mod(q, poly, d);
+        pop[i] = q;
+    }
+    std::vector<uint8_t> img(kTabBytes);
+    for (int e = 0; e < 256; e++)
+        for (int c = 0; c < kTabCopies; c++) {
+            memcpy(&img[(e << 8) | (c << 3)], &pop[e], 8);
+            memcpy(&img[kPushBase | (e << 8) | (c << 3)], &push[e], 8);
+        }
+    return img;
+}
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;  // elements
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t alloc = std::max<size_t>(want, 1);
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), alloc * sizeof(T));
+        if (e == hipSuccess) n = alloc;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+constexpr int kNumTimed = 6;
+const char* kKernelNames[kNumTimed] = {"prep", "cdc_scan", "cdc_resolve", "cdc_prefix", "cdc_scatter",
+                                       "chunk_hash"};
+
+}  // namespace
+
+struct sdfs_cdc_engine {
+    sdfs_cdc_params prm{};
+    int degree = 0;
+    int num_cus = 256;
+    uint32_t seg_len = 2048;
+    uint32_t first_off = 0;
+    uint32_t bin_shift = 0, nbins = 1;
+    uint32_t digest_len = 32;
+    hipStream_t stream = nullptr;
+    std::mutex mu;  // one engine context: calls are serialised (DESIGN.md "Host edge")
+
+    DevBuf<uint8_t> tab_image;
+    // workspace for run_device
+    DevBuf<uint32_t> bitmap;
+    DevBuf<uint64_t> seg_prefix;
+    DevBuf<uint32_t> small;  // hist[kMaxBins] | cursor[kMaxBins] | overflow[1]
+    DevBuf<uint32_t> rec_base;
+    DevBuf<uint32_t> tasks;
+    // host-path device buffers
+    DevBuf<uint8_t> h_data;
+    DevBuf<uint64_t> h_offs;
+    DevBuf<uint32_t> h_lens;
+    DevBuf<uint32_t> o_counts, o_starts, o_lens, o_total;
+    DevBuf<uint8_t> o_digests;
+    // pinned host staging
+    uint8_t* pin_data = nullptr;
+    size_t pin_data_n = 0;
+    uint8_t* pin_out = nullptr;
+    size_t pin_out_n = 0;
+
+    // per-kernel HIP events for the last `timing_slots` runs (ring); averaged by kernel_times
+    int timing_slots = 0;
+    std::vector<std::vector<hipEvent_t>> ev_runs;
+    uint64_t runs_recorded = 0;
+    hipEvent_t* ev = nullptr;  // event set of the run in flight (nullptr: timing off)
+};
+
+namespace {
+
+int validate(const sdfs_cdc_params* p) {
+    if (!p) return fail(SDFS_CDC_EINVAL, "null params");
+    const int d = poly_degree(p->poly);
+    if (d < 40 || d > 55) return fail(SDFS_CDC_EINVAL, "polynomial degree %d outside [40,55]", d);
+    if (!scan_window_supported((int)p->window))
+        return fail(SDFS_CDC_EINVAL, "window %u unsupported (16/32/48/64)", p->window);
+    if (p->max_len == 0) return fail(SDFS_CDC_EINVAL, "max_len must be > 0");
+    if (p->min_cmp > SDFS_CDC_MIN_GE) return fail(SDFS_CDC_EINVAL, "bad min_cmp");
+    if (p->hash_algo > SDFS_CDC_MD5) return fail(SDFS_CDC_EINVAL, "bad hash_algo");
+    if (p->pred_mask >> d) return fail(SDFS_CDC_EINVAL, "pred_mask has bits above the fp degree");
+    return SDFS_CDC_OK;
+}
+
+int pinned_ensure(uint8_t** p, size_t* n, size_t want) {
+    if (*p && *n >= want) return SDFS_CDC_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *n = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(p), std::max<size_t>(want, 64), hipHostMallocDefault) != hipSuccess)
+        return fail(SDFS_CDC_ENOMEM, "hipHostMalloc(%zu) failed", want);
+    *n = std::max<size_t>(want, 64);
+    return SDFS_CDC_OK;
+}
+
+uint32_t slot_cap_for(const sdfs_cdc_params& p, uint64_t len) {
+    const uint64_t shortest_cut = p.min_cmp == SDFS_CDC_MIN_GT ? (uint64_t)p.min_len + 1 : std::max<uint64_t>(p.min_len, 1);
+    const uint64_t shortest = std::min<uint64_t>(shortest_cut, p.max_len);
+    return (uint32_t)(len / shortest + 2);
+}
+
+// The device pipeline on `s`.  Caller holds e->mu and has selected the device.
+int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
+                 const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
+                 const sdfs_cdc_dev_out* out, hipStream_t s) {
+    if (!out || !out->counts || !out->starts || !out->lens || !out->digests || !out->total)
+        return fail(SDFS_CDC_EINVAL, "incomplete sdfs_cdc_dev_out");
+    if (uniform_len && (uniform_len & 63)) return fail(SDFS_CDC_EINVAL, "uniform_len must be a multiple of 64");
+    if (!uniform_len && (!d_offs || !d_lens)) return fail(SDFS_CDC_EINVAL, "offs/lens required without uniform_len");
+    if ((reinterpret_cast<uintptr_t>(d_data) & 63) != 0) return fail(SDFS_CDC_EINVAL, "d_data must be 64-byte aligned");
+    if (uniform_len) data_bytes = (uint64_t)nbuf * uniform_len;
+    if (uniform_len && out->cap < slot_cap_for(e->prm, uniform_len))
+        return fail(SDFS_CDC_ECAP, "cap %u < slot_cap %u", out->cap, slot_cap_for(e->prm, uniform_len));
+    e->ev = nullptr;
+    if (e->timing_slots > 0) e->ev = e->ev_runs[e->runs_recorded % e->timing_slots].data();
+    const bool timing = e->ev != nullptr;
+    if (timing) HIP_TRY(hipEventRecord(e->ev[0], s));
+    if (nbuf == 0) {
+        HIP_TRY(hipMemsetAsync(out->total, 0, 4, s));
+        if (timing)
+            for (int i = 1; i <= kNumTimed; i++) HIP_TRY(hipEventRecord(e->ev[i], s));
+        if (timing) e->runs_recorded++;
+        return SDFS_CDC_OK;
+    }
+    // workspace
+    const uint64_t nwords = ((data_bytes + 63) / 64) * 2 + 2;
+    HIP_TRY(e->bitmap.ensure(nwords));
+    HIP_TRY(e->small.ensure(2 * kMaxBins + 4));
+    HIP_TRY(e->rec_base.ensure(nbuf));
+    const uint64_t nslots = (uint64_t)nbuf * out->cap;
+    HIP_TRY(e->tasks.ensure(nslots));
+    uint32_t* hist = e->small.p;
+    uint32_t* cursor = e->small.p + kMaxBins;
+    uint32_t* overflow = e->small.p + 2 * kMaxBins;
+    HIP_TRY(hipMemsetAsync(e->small.p, 0, (2 * kMaxBins + 4) * sizeof(uint32_t), s));
+
+    ScanArgs sa{};
+    sa.data = d_data;
+    sa.offs = d_offs;
+    sa.lens = d_lens;
+    sa.bitmap = e->bitmap.p;
+    sa.nbuf = nbuf;
+    sa.uniform_len = uniform_len;
+    sa.seg_len = e->seg_len;
+    sa.jshift = (uint32_t)(e->degree - 40);
+    sa.mask_lo = (uint32_t)e->prm.pred_mask;
+    sa.mask_hi = (uint32_t)(e->prm.pred_mask >> 32);
+    sa.val_lo = (uint32_t)e->prm.pred_value;
+    sa.val_hi = (uint32_t)(e->prm.pred_value >> 32);
+    sa.tab_image = e->tab_image.p;
+    uint64_t seg_bound;
+    if (uniform_len) {
+        const uint64_t spb = (uniform_len + e->seg_len - 1) / e->seg_len;
+        sa.total_segs = spb * nbuf;
+        seg_bound = sa.total_segs;
+    } else {
+        HIP_TRY(e->seg_prefix.ensure((uint64_t)nbuf + 1));
+        HIP_TRY(launch_seg_prefix(d_lens, nbuf, e->seg_len, e->seg_prefix.p, s));
+        sa.seg_prefix = e->seg_prefix.p;
+        seg_bound = data_bytes / e->seg_len + nbuf;
+    }
+    if (timing) HIP_TRY(hipEventRecord(e->ev[1], s));
+    const uint64_t per_block = (uint64_t)kScanThreads * kScanChains;
+    uint64_t grid = (seg_bound + per_block - 1) / per_block;
+    grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus);
+    grid = std::max<uint64_t>(grid, 1);
+    const bool pred64 = (e->prm.pred_mask >> 32) != 0;
+    HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, (int)grid, s));
+    if (timing) HIP_TRY(hipEventRecord(e->ev[2], s));
+
+    ResolveArgs ra{};
+    ra.bitmap = e->bitmap.p;
+    ra.offs = d_offs;
+    ra.lens = d_lens;
+    ra.nbuf = nbuf;
+    ra.uniform_len = uniform_len;
+    ra.first_off = e->first_off;
+    ra.max_len = e->prm.max_len;
+    ra.cap = out->cap;
+    ra.bin_shift = e->bin_shift;
+    ra.nbins = e->nbins;
+    ra.counts = out->counts;
+    ra.starts = out->starts;
+    ra.clens = out->lens;
+    ra.hist = hist;
+    ra.overflow = overflow;
+    HIP_TRY(launch_resolve(ra, s));
+    if (timing) HIP_TRY(hipEventRecord(e->ev[3], s));
+
+    PrefixArgs pa{};
+    pa.counts = out->counts;
+    pa.nbuf = nbuf;
+    pa.hist = hist;
+    pa.nbins = e->nbins;
+    pa.cursor = cursor;
+    pa.rec_base = e->rec_base.p;
+    pa.total = out->total;
+    HIP_TRY(launch_prefix(pa, s));
+    if (timing) HIP_TRY(hipEventRecord(e->ev[4], s));
+
+    ScatterArgs ca{};
+    ca.counts = out->counts;
+    ca.clens = out->lens;
+    ca.nbuf = nbuf;
+    ca.cap = out->cap;
+    ca.bin_shift = e->bin_shift;
+    ca.nbins = e->nbins;
+    ca.cursor = cursor;
+    ca.tasks = e->tasks.p;
+    HIP_TRY(launch_scatter(ca, s));
+    if (timing) HIP_TRY(hipEventRecord(e->ev[5], s));
+
+    HashArgs ha{};
+    ha.data = d_data;
+    ha.offs = d_offs;
+    ha.uniform_len = uniform_len;
+    ha.tasks = e->tasks.p;
+    ha.total = out->total;
+    ha.starts = out->starts;
+    ha.clens = out->lens;
+    ha.rec_base = e->rec_base.p;
+    ha.cap = out->cap;
+    ha.digests = out->digests;
+    ha.records = out->records;
+    ha.records_cap = out->records_cap;
+    ha.buffer_id_base = buffer_id_base;
+    ha.algo = e->prm.hash_algo;
+    // upper bound on chunks: every buffer at most cap
+    HIP_TRY(launch_hash(ha, nslots, s));
+    if (timing) {
+        HIP_TRY(hipEventRecord(e->ev[6], s));
+        e->runs_recorded++;
+    }
+    return SDFS_CDC_OK;
+}
+
+// Host buffers -> device, pipeline, device -> host.  Caller holds e->mu.
+int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t nbuf,
+               uint32_t* counts, uint32_t* starts, uint32_t* lens_out, uint8_t* digests, uint32_t cap) {
+    if (nbuf == 0) return SDFS_CDC_OK;
+    const uint64_t staging = e->prm.max_batch_bytes ? e->prm.max_batch_bytes : (256ull << 20);
+    uint32_t b0 = 0;
+    while (b0 < nbuf) {
+        // pack as many buffers as fit (at 64-byte aligned offsets)
+        uint64_t bytes = 0;
+        uint32_t b1 = b0;
+        uint64_t maxlen = 1;
+        while (b1 < nbuf) {
+            const uint64_t need = (lens[b1] + 63ull) & ~63ull;
+            if (b1 > b0 && bytes + need > staging) break;
+            bytes += need;
+            maxlen = std::max<uint64_t>(maxlen, lens[b1]);
+            b1++;
+        }
+        const uint32_t n = b1 - b0;
+        const uint32_t dcap = slot_cap_for(e->prm, maxlen);
+        int rc = pinned_ensure(&e->pin_data, &e->pin_data_n, bytes + n * 12ull + 64);
+        if (rc) return rc;
+        uint64_t* hoffs = reinterpret_cast<uint64_t*>(e->pin_data + ((bytes + 63) & ~63ull));
+        uint32_t* hlens = reinterpret_cast<uint32_t*>(hoffs + n);
+        uint64_t o = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            memcpy(e->pin_data + o, base + offs[b0 + i], lens[b0 + i]);
+            hoffs[i] = o;
+            hlens[i] = lens[b0 + i];
+            o += (lens[b0 + i] + 63ull) & ~63ull;
+        }
+        HIP_TRY(e->h_data.ensure(std::max<uint64_t>(bytes, 64)));
+        HIP_TRY(e->h_offs.ensure(n));
+        HIP_TRY(e->h_lens.ensure(n));
+        HIP_TRY(e->o_counts.ensure(n));
+        HIP_TRY(e->o_starts.ensure((uint64_t)n * dcap));
+        HIP_TRY(e->o_lens.ensure((uint64_t)n * dcap));
+        HIP_TRY(e->o_digests.ensure((uint64_t)n * dcap * 32));
+        HIP_TRY(e->o_total.ensure(1));
+        hipStream_t s = e->stream;
+        HIP_TRY(hipMemcpyAsync(e->h_data.p, e->pin_data, bytes, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(e->h_offs.p, hoffs, n * 8ull, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(e->h_lens.p, hlens, n * 4ull, hipMemcpyHostToDevice, s));
+        sdfs_cdc_dev_out out{};
+        out.counts = e->o_counts.p;
+        out.starts = e->o_starts.p;
+        out.lens = e->o_lens.p;
+        out.digests = e->o_digests.p;
+        out.cap = dcap;
+        out.total = e->o_total.p;
+        rc = run_pipeline(e, e->h_data.p, bytes, e->h_offs.p, e->h_lens.p, n, 0, 0, &out, s);
+        if (rc) return rc;
+        // results back through pinned memory
+        const uint64_t nout = (uint64_t)n * dcap;
+        const size_t out_bytes = n * 4ull + nout * 8 + nout * 32 + 64;
+        rc = pinned_ensure(&e->pin_out, &e->pin_out_n, out_bytes);
+        if (rc) return rc;
+        uint32_t* pc = reinterpret_cast<uint32_t*>(e->pin_out);
+        uint32_t* ps = pc + n;
+        uint32_t* pl = ps + nout;
+        uint8_t* pd = reinterpret_cast<uint8_t*>(pl + nout);
+        HIP_TRY(hipMemcpyAsync(pc, out.counts, n * 4ull, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(ps, out.starts, nout * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(pl, out.lens, nout * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(pd, out.digests, nout * 32, hipMemcpyDeviceToHost, s));
+        uint32_t ovf = 0;
+        HIP_TRY(hipMemcpyAsync(&ovf, e->small.p + 2 * kMaxBins, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (ovf) return fail(SDFS_CDC_EHIP, "internal: chunk slot overflow");
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t c = pc[i];
+            if (c > cap) return fail(SDFS_CDC_ECAP, "buffer %u has %u chunks > cap %u", b0 + i, c, cap);
+            counts[b0 + i] = c;
+            const uint64_t so = (uint64_t)i * dcap, dst = (uint64_t)(b0 + i) * cap;
+            memcpy(starts + dst, ps + so, c * 4ull);
+            memcpy(lens_out + dst, pl + so, c * 4ull);
+            if (digests)
+                for (uint32_t k = 0; k < c; k++)
+                    memcpy(digests + (dst + k) * e->digest_len, pd + (so + k) * 32, e->digest_len);
+        }
+        b0 = b1;
+    }
+    return SDFS_CDC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdfs_cdc_abi_version(void) { return SDFS_CDC_ABI_VERSION; }
+
+const char* sdfs_cdc_last_error(void) { return g_last_error.c_str(); }
+
+int sdfs_cdc_params_default(sdfs_cdc_params* p, int backup_volume) {
+    if (!p) return fail(SDFS_CDC_EINVAL, "null params");
+    memset(p, 0, sizeof(*p));
+    p->poly = 10923124345206883ull;                        // VariableSha256HashEngine.java:41
+    p->window = 48;                                        // HashFunctionPool.java:51
+    p->min_len = 4 * 1024 - 1;                             // Main.java:189
+    p->max_len = backup_volume ? 128 * 1024 : 32 * 1024;   // VolumeConfigWriter.java:96,301
+    p->chunk_length = backup_volume ? 40960u * 1024 : 256u * 1024;  // VolumeConfigWriter.java:63,304
+    p->pred_mask = 0xFFF;                                  // SURVEY.md A.3 (knob; parity unpinned)
+    p->pred_value = 0;
+    p->min_cmp = SDFS_CDC_MIN_GT;
+    p->hash_algo = SDFS_CDC_SHA256;                        // VolumeConfigWriter.java:109
+    p->device = 0;
+    p->max_batch_bytes = 0;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
+    if (!out) return fail(SDFS_CDC_EINVAL, "null out");
+    *out = nullptr;
+    int rc = validate(p);
+    if (rc) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SDFS_CDC_ENODEV, "no HIP device");
+    if (p->device < 0 || p->device >= ndev) return fail(SDFS_CDC_ENODEV, "device %d of %d", p->device, ndev);
+    HIP_TRY(hipSetDevice(p->device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, p->device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SDFS_CDC_ENODEV, "device %d is %s, this build targets gfx950", p->device, prop.gcnArchName);
+    auto* e = new sdfs_cdc_engine();
+    e->prm = *p;
+    e->degree = poly_degree(p->poly);
+    e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    e->first_off = p->min_cmp == SDFS_CDC_MIN_GT ? p->min_len : (p->min_len ? p->min_len - 1 : 0);
+    e->digest_len = p->hash_algo == SDFS_CDC_SHA256 ? 32 : (p->hash_algo == SDFS_CDC_SHA256_160 ? 20 : 16);
+    // bins over SHA block counts: maxLen chunk = (max_len + 8)/64 + 1 blocks
+    const uint32_t maxblocks = (p->max_len + 8) / 64 + 1;
+    e->bin_shift = 0;
+    while ((maxblocks >> e->bin_shift) >= (uint32_t)kMaxBins) e->bin_shift++;
+    e->nbins = (maxblocks >> e->bin_shift) + 1;
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return fail(SDFS_CDC_EHIP, "hipStreamCreate failed");
+    }
+    std::vector<uint8_t> img = build_table_image(p->poly, p->window);
+    if (e->tab_image.ensure(kTabBytes) != hipSuccess ||
+        hipMemcpy(e->tab_image.p, img.data(), kTabBytes, hipMemcpyHostToDevice) != hipSuccess) {
+        sdfs_cdc_destroy(e);
+        return fail(SDFS_CDC_ENOMEM, "table upload failed");
+    }
+    *out = e;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
+    if (!e) return SDFS_CDC_OK;
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        (void)hipSetDevice(e->prm.device);
+        if (e->stream) (void)hipStreamSynchronize(e->stream);
+        e->tab_image.release();
+        e->bitmap.release();
+        e->seg_prefix.release();
+        e->small.release();
+        e->rec_base.release();
+        e->tasks.release();
+        e->h_data.release();
+        e->h_offs.release();
+        e->h_lens.release();
+        e->o_counts.release();
+        e->o_starts.release();
+        e->o_lens.release();
+        e->o_total.release();
+        e->o_digests.release();
+        if (e->pin_data) (void)hipHostFree(e->pin_data);
+        if (e->pin_out) (void)hipHostFree(e->pin_out);
+        for (auto& run : e->ev_runs)
+            for (auto& ev : run)
+                if (ev) (void)hipEventDestroy(ev);
+        if (e->stream) (void)hipStreamDestroy(e->stream);
+    }
+    delete e;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_is_variable_length(const sdfs_cdc_engine*) { return 1; }
+int sdfs_cdc_get_max_len(const sdfs_cdc_engine* e) { return e ? (int)e->prm.chunk_length : -1; }
+int sdfs_cdc_get_min_len(const sdfs_cdc_engine* e) { return e ? (int)e->prm.min_len : -1; }
+int sdfs_cdc_set_seed(sdfs_cdc_engine*, int) { return SDFS_CDC_OK; }
+int sdfs_cdc_digest_len(const sdfs_cdc_engine* e) { return e ? (int)e->digest_len : -1; }
+uint32_t sdfs_cdc_slot_cap(const sdfs_cdc_engine* e, uint64_t buf_len) { return e ? slot_cap_for(e->prm, buf_len) : 0; }
+
+int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
+                        uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base, const sdfs_cdc_dev_out* out,
+                        void* stream) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    if (!uniform_len)
+        return fail(SDFS_CDC_EINVAL, "sdfs_cdc_run_device: ragged layouts need sdfs_cdc_run_device_ragged");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e->stream;
+    return run_pipeline(e, d_data, 0, d_offs, d_lens, nbuf, uniform_len, buffer_id_base, out, s);
+}
+
+int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
+                               const uint32_t* d_lens, uint32_t nbuf, uint64_t buffer_id_base,
+                               const sdfs_cdc_dev_out* out, void* stream) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e->stream;
+    return run_pipeline(e, d_data, data_bytes, d_offs, d_lens, nbuf, 0, buffer_id_base, out, s);
+}
+
+int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    if (nruns < 0 || nruns > 4096) return fail(SDFS_CDC_EINVAL, "timing slots %d", nruns);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    while ((int)e->ev_runs.size() < nruns) {
+        std::vector<hipEvent_t> run(kNumTimed + 1, nullptr);
+        for (auto& ev : run) HIP_TRY(hipEventCreate(&ev));
+        e->ev_runs.push_back(std::move(run));
+    }
+    e->timing_slots = nruns;
+    e->runs_recorded = 0;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int n) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    if (e->timing_slots == 0 || e->runs_recorded == 0) return 0;
+    const uint64_t nr = std::min<uint64_t>(e->runs_recorded, (uint64_t)e->timing_slots);
+    int k = 0;
+    for (int i = 0; i < kNumTimed && k < n; i++, k++) {
+        double sum = 0;
+        for (uint64_t r = 0; r < nr; r++) {
+            auto& run = e->ev_runs[(e->runs_recorded - 1 - r) % e->timing_slots];
+            HIP_TRY(hipEventSynchronize(run[i + 1]));
+            float t = 0;
+            HIP_TRY(hipEventElapsedTime(&t, run[i], run[i + 1]));
+            sum += t;
+        }
+        if (names) names[k] = kKernelNames[i];
+        if (ms) ms[k] = (float)(sum / nr);
+    }
+    return k;
+}
+
+int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
+                              uint32_t nbuf, uint32_t* counts, uint32_t* starts, uint32_t* lens_out,
+                              uint8_t* digests, uint32_t cap) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    if (nbuf && (!base || !offs || !lens || !counts || !starts || !lens_out))
+        return fail(SDFS_CDC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    return host_batch(e, base, offs, lens, nbuf, counts, starts, lens_out, digests, cap);
+}
+
+int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, uint32_t* starts, uint32_t* lens,
+                        uint8_t* digests, uint32_t cap, uint32_t* count) {
+    if (!e || !count) return fail(SDFS_CDC_EINVAL, "null argument");
+    *count = 0;
+    if (len == 0) return SDFS_CDC_OK;  // an empty byte[] yields no Finger
+    if (!buf) return fail(SDFS_CDC_EINVAL, "null buffer");
+    const uint64_t off = 0;
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    return host_batch(e, buf, &off, &len, 1, count, starts, lens, digests, cap);
+}
+
+int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest) {
+    if (!e || !digest || (len && !data)) return fail(SDFS_CDC_EINVAL, "null argument");
+    if (len > 0xFFFFFFFFull) return fail(SDFS_CDC_EINVAL, "getHash input > 4 GiB");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    hipStream_t s = e->stream;
+    int rc = pinned_ensure(&e->pin_data, &e->pin_data_n, len + 256);
+    if (rc) return rc;
+    if (len) memcpy(e->pin_data, data, len);
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(e->pin_data + ((len + 63) & ~63ull));
+    ctl[0] = 0;                  // starts[0]
+    ctl[1] = (uint32_t)len;      // lens[0]
+    ctl[2] = 0;                  // tasks[0]
+    ctl[3] = 1;                  // total
+    HIP_TRY(e->h_data.ensure(std::max<uint64_t>(len, 64) + 64));
+    HIP_TRY(e->o_starts.ensure(4));
+    HIP_TRY(e->o_digests.ensure(32));
+    if (len) HIP_TRY(hipMemcpyAsync(e->h_data.p, e->pin_data, len, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->o_starts.p, ctl, 16, hipMemcpyHostToDevice, s));
+    HashArgs ha{};
+    ha.data = e->h_data.p;
+    ha.uniform_len = 64;  // buffer 0 at offset 0
+    ha.starts = e->o_starts.p;
+    ha.clens = e->o_starts.p + 1;
+    ha.tasks = e->o_starts.p + 2;
+    ha.total = e->o_starts.p + 3;
+    ha.cap = 1;
+    ha.digests = e->o_digests.p;
+    ha.algo = e->prm.hash_algo;
+    HIP_TRY(launch_hash(ha, 1, s));
+    HIP_TRY(hipMemcpyAsync(ctl + 4, e->o_digests.p, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    memcpy(digest, ctl + 4, e->digest_len);
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_synth_device(sdfs_cdc_engine* e, uint8_t* d_out, uint64_t n, uint64_t seed, uint64_t stream,
+                          uint64_t offset, void* stream_handle) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    HIP_TRY(hipSetDevice(e->prm.device));
+    hipStream_t s = stream_handle ? reinterpret_cast<hipStream_t>(stream_handle) : e->stream;
+    HIP_TRY(launch_synth(d_out, n, seed, stream, offset, s));
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_stream_sync(sdfs_cdc_engine* e) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    HIP_TRY(hipSetDevice(e->prm.device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return SDFS_CDC_OK;
+}
+
+}  // extern "C"

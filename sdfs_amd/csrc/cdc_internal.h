@@ -1,0 +1,113 @@
+// cdc_internal.h — device-side layout shared by the kernels (cdc_kernels.hip) and the engine
+// (cdc_engine.hip).  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdfs {
+
+// LDS image of the rolling-hash tables (DESIGN.md "Rabin scan"): 32 lane-private copies so that
+// every ds_read_b64 of a 32-lane group hits 32 distinct bank pairs (conflict-free for random
+// indices).  pop table at [0, 64K): entry o, copy c at byte (o << 8) | (c << 3);
+// push table at [64K, 128K): entry j, copy c at 0x10000 | (j << 8) | (c << 3).
+constexpr int kTabCopies = 32;
+constexpr int kTabBytes = 2 * 256 * kTabCopies * 8;  // 131072
+constexpr int kPushBase = 0x10000;
+
+constexpr int kScanThreads = 1024;  // one workgroup per CU (128 KiB LDS)
+constexpr int kScanChains = 2;      // independent segments per lane (ILP across the LDS latency)
+
+constexpr int kMaxBins = 512;  // SHA work binning by block count (DESIGN.md "Load balance")
+constexpr int kRecordBytes = 48;
+
+struct ScanArgs {
+    const uint8_t* data;
+    const uint64_t* offs;        // general layout (nullptr when uniform)
+    const uint32_t* lens;
+    const uint64_t* seg_prefix;  // [nbuf+1] segment prefix (general layout)
+    uint32_t* bitmap;            // 1 bit per byte position, bit i of word w = position 32w+i
+    uint64_t total_segs;
+    uint32_t nbuf;
+    uint32_t uniform_len;        // != 0 -> uniform layout
+    uint32_t seg_len;            // bytes per segment, multiple of 64
+    uint32_t jshift;             // deg(P) - 40 : bit offset of the push index inside the hi word
+    uint32_t mask_lo, mask_hi, val_lo, val_hi;
+    const uint8_t* tab_image;    // kTabBytes, global copy of the LDS image
+};
+
+struct ResolveArgs {
+    const uint32_t* bitmap;
+    const uint64_t* offs;
+    const uint32_t* lens;
+    uint32_t nbuf;
+    uint32_t uniform_len;
+    uint32_t first_off;  // min_len (n > min) or min_len-1 (n >= min): first cut offset allowed
+    uint32_t max_len;
+    uint32_t cap;        // slots per buffer
+    uint32_t bin_shift;
+    uint32_t nbins;
+    uint32_t* counts;
+    uint32_t* starts;
+    uint32_t* clens;
+    uint32_t* hist;      // [nbins]
+    uint32_t* overflow;  // [1] set when a buffer needs more than cap slots
+};
+
+struct PrefixArgs {
+    const uint32_t* counts;
+    uint32_t nbuf;
+    const uint32_t* hist;
+    uint32_t nbins;
+    uint32_t* cursor;     // [nbins] exclusive prefix, descending bin order
+    uint32_t* rec_base;   // [nbuf] exclusive prefix of counts
+    uint32_t* total;      // [1]
+};
+
+struct ScatterArgs {
+    const uint32_t* counts;
+    const uint32_t* clens;
+    uint32_t nbuf;
+    uint32_t cap;
+    uint32_t bin_shift;
+    uint32_t nbins;
+    uint32_t* cursor;
+    uint32_t* tasks;
+};
+
+struct HashArgs {
+    const uint8_t* data;
+    const uint64_t* offs;
+    uint32_t uniform_len;
+    const uint32_t* tasks;     // slot indices, longest first
+    const uint32_t* total;     // [1] number of tasks
+    const uint32_t* starts;
+    const uint32_t* clens;
+    const uint32_t* rec_base;  // may be null when records == null
+    uint32_t cap;
+    uint8_t* digests;          // [slot*32]
+    uint8_t* records;          // optional dense table
+    uint64_t records_cap;
+    uint64_t buffer_id_base;
+    uint32_t algo;             // SDFS_CDC_SHA256 / _SHA256_160 / _MD5
+};
+
+inline uint64_t splitmix64_host(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// kernel launchers (cdc_kernels.hip); all asynchronous on `stream`
+hipError_t launch_seg_prefix(const uint32_t* lens, uint32_t nbuf, uint32_t seg_len, uint64_t* seg_prefix,
+                             hipStream_t stream);
+hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int grid, hipStream_t stream);
+hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
+hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
+hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);
+hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, hipStream_t stream);
+hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
+                        hipStream_t stream);
+bool scan_window_supported(int window);
+
+}  // namespace sdfs

@@ -1,0 +1,695 @@
+// cdc_kernels.hip — hand-written CDNA4 (gfx950) kernels for SDFS variable-block CDC + fingerprint.
+//
+// Pipeline per batch of write buffers (DESIGN.md "Kernels"):
+//   1. cdc_scan     windowed Rabin rolling hash over every byte -> candidate bitmap (1 bit/byte)
+//   2. cdc_resolve  greedy cut resolution per buffer (min/max rules) -> (start,len) slots
+//   3. cdc_prefix   bin cursors (longest-first) + per-buffer record bases + total
+//   4. cdc_scatter  chunk slots -> task list sorted by SHA block count (load balance)
+//   5. chunk_hash   one lane per chunk: SHA-256 / MD5 over the chunk bytes -> digests, records
+//
+// Reference semantics: VariableSha256HashEngine.getChunks (VariableSha256HashEngine.java:71-86)
+// driving the rabinwindow EnhancedFingerFactory loop; getHash (:58-67).
+// Integer/bit work only: no MFMA (DESIGN.md explains the VALU roofline).
+#include "cdc_internal.h"
+
+namespace sdfs {
+
+// gfx950 has no v_xor3_b32, but it has v_bitop3_b32 (any 3-input boolean function, truth table
+// 0x96 = a^b^c, 0xE8 = majority); hipcc does not form it for xor chains on its own.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
+// ------------------------------------------------------------------------------------------
+// 1. candidate scan
+// ------------------------------------------------------------------------------------------
+// One rolling step for byte `inb` (taken from byte p of dword `dw`), popping the byte that left
+// the window (byte q of dword `odw`).  fp = hi:lo (deg < 56).  Equivalent to the jar's
+// pushByte/popByte pair:
+//   j = (fp >> (d-8)) & 0xFF;  fp = ((fp << 8) | b) ^ push[j];  fp ^= pop[o]
+// push[j] carries j*x^d, which cancels the 8 bits shifted above deg-1.
+template <int P, int Q>
+__device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
+                                          uint32_t push_base, uint32_t jshift, const uint8_t* tab) {
+    const uint32_t j = __builtin_amdgcn_ubfe(hi, jshift, 8);
+    const uint32_t pa = (j << 8) | push_base;                                          // push[j], lane copy
+    const uint32_t qa = __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + Q) << 8));  // (o << 8) | c8
+    const uint2 pv = *reinterpret_cast<const uint2*>(tab + pa);
+    const uint2 qv = *reinterpret_cast<const uint2*>(tab + qa);
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);             // (fp << 8) >> 32
+    const uint32_t nlo = __builtin_amdgcn_perm(lo, dw, 0x06050400u | P);     // (lo << 8) | b
+    lo = xor3(nlo, pv.x, qv.x);
+    hi = xor3(nhi, pv.y, qv.y);
+}
+
+// push-only step (window warm-up from the zero state; no byte leaves the window yet)
+template <int P>
+__device__ __forceinline__ void push_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t push_base,
+                                          uint32_t jshift, const uint8_t* tab) {
+    const uint32_t j = __builtin_amdgcn_ubfe(hi, jshift, 8);
+    const uint2 pv = *reinterpret_cast<const uint2*>(tab + ((j << 8) | push_base));
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);
+    const uint32_t nlo = __builtin_amdgcn_perm(lo, dw, 0x06050400u | P);
+    lo = nlo ^ pv.x;
+    hi = nhi ^ pv.y;
+}
+
+template <bool PRED64>
+__device__ __forceinline__ uint32_t cand_bit(uint32_t lo, uint32_t hi, const ScanArgs& a) {
+    if constexpr (PRED64)
+        return ((lo & a.mask_lo) == a.val_lo) & ((hi & a.mask_hi) == a.val_hi);
+    else
+        return (lo & a.mask_lo) == a.val_lo;
+}
+
+// Byte o of the current 64-byte block, with the byte that leaves the window at o - W
+// (in this block when o >= W, otherwise in the previous block).
+template <int W, bool PRED64, int O>
+__device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& bits, const uint32_t (&cur)[16],
+                                          const uint32_t (&prev)[16], uint32_t c8, uint32_t push_base,
+                                          const uint8_t* tab, const ScanArgs& a) {
+    constexpr int OLD = O - W;  // may be negative -> previous block
+    constexpr int OI = OLD >= 0 ? OLD : OLD + 64;
+    const uint32_t odw = OLD >= 0 ? cur[OI >> 2] : prev[OI >> 2];
+    roll_step<(O & 3), (OI & 3)>(lo, hi, cur[O >> 2], odw, c8, push_base, a.jshift, tab);
+    bits |= cand_bit<PRED64>(lo, hi, a) << (O & 31);
+}
+
+#ifndef SDFS_SCAN_SCHED_GROUP
+#define SDFS_SCAN_SCHED_GROUP 4
+#endif
+constexpr int kSchedGroup = SDFS_SCAN_SCHED_GROUP;  // bytes per scheduling region
+
+template <int W, bool PRED64, int O, int NCH>
+__device__ __forceinline__ void bytes_from(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
+                                           const uint32_t (&cur)[NCH][16], const uint32_t (&prev)[NCH][16],
+                                           uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
+    if constexpr (O < 32) {
+#pragma unroll
+        for (int c = 0; c < NCH; c++) byte_step<W, PRED64, O>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
+        // keep the scheduler from hoisting every (chain-independent) pop read of the block
+        // ahead of the rolling chain: that costs ~2 VGPRs per byte and spills.
+        if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) __builtin_amdgcn_sched_barrier(0);
+        bytes_from<W, PRED64, O + 1, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+    }
+}
+template <int W, bool PRED64, int O, int NCH>
+__device__ __forceinline__ void bytes_from_hi(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
+                                              const uint32_t (&cur)[NCH][16], const uint32_t (&prev)[NCH][16],
+                                              uint32_t c8, uint32_t push_base, const uint8_t* tab,
+                                              const ScanArgs& a) {
+    if constexpr (O < 64) {
+#pragma unroll
+        for (int c = 0; c < NCH; c++) byte_step<W, PRED64, O>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
+        if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) __builtin_amdgcn_sched_barrier(0);
+        bytes_from_hi<W, PRED64, O + 1, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+    }
+}
+
+template <int W, int O>
+__device__ __forceinline__ void warm_from(uint32_t& lo, uint32_t& hi, const uint32_t (&prev)[16], uint32_t push_base,
+                                          uint32_t jshift, const uint8_t* tab) {
+    if constexpr (O < 64) {
+        push_step<(O & 3)>(lo, hi, prev[O >> 2], push_base, jshift, tab);
+        warm_from<W, O + 1>(lo, hi, prev, push_base, jshift, tab);
+    }
+}
+
+// Load the 64-byte block at byte address `addr` if it is readable up to `lim`; dwords that hold
+// no byte below `lim` read as zero (only the buffer's last block takes the guarded path).
+__device__ __forceinline__ void load_block(uint32_t (&d)[16], const uint8_t* data, uint64_t addr, uint64_t lim) {
+    const bool full = addr + 64 <= lim;
+    if (__all(full)) {
+        const uint4* p = reinterpret_cast<const uint4*>(data + addr);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint4 v = p[i];
+            d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+        }
+    } else {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(data + addr);
+#pragma unroll
+        for (int i = 0; i < 16; i++) d[i] = (addr + 4 * i < lim) ? p[i] : 0u;
+    }
+}
+
+template <int W, bool PRED64>
+__global__ __launch_bounds__(kScanThreads) void cdc_scan_kernel(ScanArgs a) {
+    constexpr int NCH = kScanChains;
+    __shared__ __attribute__((aligned(16))) uint8_t tab[kTabBytes];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.tab_image);
+        uint4* dst = reinterpret_cast<uint4*>(tab);
+        for (int i = threadIdx.x; i < kTabBytes / 16; i += kScanThreads) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c8 = (lane & 31) << 3;
+    const uint32_t push_base = kPushBase | c8;
+    const uint64_t total = a.uniform_len ? a.total_segs : a.seg_prefix[a.nbuf];
+    const uint64_t per_iter = (uint64_t)kScanThreads * NCH;
+
+    for (uint64_t base = (uint64_t)blockIdx.x * per_iter; base < total; base += (uint64_t)gridDim.x * per_iter) {
+        uint64_t start[NCH], end[NCH];
+        uint32_t nblk[NCH];
+        bool first[NCH];
+        uint32_t maxblk = 0;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const uint64_t seg = base + (uint64_t)c * kScanThreads + threadIdx.x;
+            start[c] = end[c] = 0;
+            nblk[c] = 0;
+            first[c] = true;
+            if (seg < total) {
+                uint64_t bstart, blen, s;
+                if (a.uniform_len) {
+                    const uint64_t spb = (a.uniform_len + a.seg_len - 1) / a.seg_len;
+                    const uint64_t b = seg / spb;
+                    s = seg - b * spb;
+                    bstart = b * a.uniform_len;
+                    blen = a.uniform_len;
+                } else {
+                    uint32_t lo_b = 0, hi_b = a.nbuf;  // last b with seg_prefix[b] <= seg
+                    while (hi_b - lo_b > 1) {
+                        const uint32_t mid = (lo_b + hi_b) >> 1;
+                        if (a.seg_prefix[mid] <= seg) lo_b = mid; else hi_b = mid;
+                    }
+                    s = seg - a.seg_prefix[lo_b];
+                    bstart = a.offs[lo_b];
+                    blen = a.lens[lo_b];
+                }
+                start[c] = bstart + s * a.seg_len;
+                const uint64_t bend = bstart + blen;
+                end[c] = start[c] + a.seg_len < bend ? start[c] + a.seg_len : bend;
+                nblk[c] = (uint32_t)((end[c] - start[c] + 63) >> 6);
+                // window warm-up needs the previous block unless this is the buffer's first segment
+                first[c] = start[c] == bstart;
+            }
+            maxblk = nblk[c] > maxblk ? nblk[c] : maxblk;
+        }
+
+        uint32_t lo[NCH], hi[NCH];
+        uint32_t prev[NCH][16], cur[NCH][16];
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            if (nblk[c] != 0 && !first[c]) {
+                load_block(prev[c], a.data, start[c] - 64, start[c]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; i++) prev[c][i] = 0;  // bytes before the buffer are empty
+            }
+            lo[c] = hi[c] = 0;
+            warm_from<W, 64 - W>(lo[c], hi[c], prev[c], push_base, a.jshift, tab);
+        }
+
+        for (uint32_t blk = 0; blk < maxblk; blk++) {
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                const bool act = blk < nblk[c];
+                const uint64_t addr = act ? start[c] + 64ull * blk : 0;
+                load_block(cur[c], a.data, addr, act ? end[c] : 0);
+            }
+            uint32_t bits[NCH];
+#pragma unroll
+            for (int c = 0; c < NCH; c++) bits[c] = 0;
+            bytes_from<W, PRED64, 0, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+            uint32_t w0[NCH];
+#pragma unroll
+            for (int c = 0; c < NCH; c++) { w0[c] = bits[c]; bits[c] = 0; }
+            bytes_from_hi<W, PRED64, 32, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                if (blk < nblk[c]) {
+                    const uint64_t pos = start[c] + 64ull * blk;
+                    *reinterpret_cast<uint2*>(a.bitmap + (pos >> 5)) = make_uint2(w0[c], bits[c]);
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i++) prev[c][i] = cur[c][i];
+            }
+        }
+    }
+}
+
+bool scan_window_supported(int window) {
+    return window == 16 || window == 32 || window == 48 || window == 64;
+}
+
+template <int W>
+static hipError_t launch_scan_w(const ScanArgs& a, bool pred64, int grid, hipStream_t s) {
+    if (pred64)
+        hipLaunchKernelGGL((cdc_scan_kernel<W, true>), dim3(grid), dim3(kScanThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((cdc_scan_kernel<W, false>), dim3(grid), dim3(kScanThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int grid, hipStream_t s) {
+    switch (window) {
+    case 16: return launch_scan_w<16>(a, pred64, grid, s);
+    case 32: return launch_scan_w<32>(a, pred64, grid, s);
+    case 48: return launch_scan_w<48>(a, pred64, grid, s);
+    case 64: return launch_scan_w<64>(a, pred64, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// segment prefix for the general (ragged) layout: seg_prefix[b] = sum_{b'<b} ceil(len/seg_len)
+__global__ __launch_bounds__(1024) void seg_prefix_kernel(const uint32_t* lens, uint32_t nbuf, uint32_t seg_len,
+                                                          uint64_t* seg_prefix) {
+    __shared__ uint64_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nbuf + 1023) / 1024;
+    const uint32_t b0 = t * per, b1 = (b0 + per < nbuf) ? b0 + per : nbuf;
+    uint64_t sum = 0;
+    for (uint32_t b = b0; b < b1; b++) sum += (lens[b] + seg_len - 1) / seg_len;
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint64_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;
+    for (uint32_t b = b0; b < b1; b++) {
+        seg_prefix[b] = run;
+        run += (lens[b] + seg_len - 1) / seg_len;
+    }
+    if (t == 1023) seg_prefix[nbuf] = part[1023];
+}
+
+hipError_t launch_seg_prefix(const uint32_t* lens, uint32_t nbuf, uint32_t seg_len, uint64_t* seg_prefix,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(seg_prefix_kernel, dim3(1), dim3(1024), 0, s, lens, nbuf, seg_len, seg_prefix);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// 2. cut resolution: one wave per buffer, ballot search over 64 bitmap words (2048 positions)
+// ------------------------------------------------------------------------------------------
+// First candidate position in [lo, hi] (buffer-relative), or -1.
+__device__ __forceinline__ int64_t find_first(const uint32_t* bm, uint64_t word0, uint64_t lo, uint64_t hi,
+                                              uint32_t lane) {
+    const uint64_t wlo = lo >> 5, whi = hi >> 5;
+    for (uint64_t wb = wlo; wb <= whi; wb += 64) {
+        const uint64_t w = wb + lane;
+        uint32_t bits = 0;
+        if (w <= whi) {
+            bits = bm[word0 + w];
+            if (w == wlo) bits &= ~0u << (lo & 31);
+            if (w == whi) bits &= (hi & 31) == 31 ? ~0u : ((2u << (hi & 31)) - 1u);
+        }
+        const uint64_t m = __ballot(bits != 0);
+        if (m) {
+            const uint32_t l = __builtin_ctzll(m);
+            const uint32_t b = __shfl(bits, l);
+            return (int64_t)((wb + l) * 32 + __builtin_ctz(b));
+        }
+    }
+    return -1;
+}
+
+__device__ __forceinline__ uint32_t sha_blocks(uint32_t len) { return (len + 8) / 64 + 1; }
+
+__global__ __launch_bounds__(256) void cdc_resolve_kernel(ResolveArgs a) {
+    __shared__ uint32_t lhist[kMaxBins];
+    for (uint32_t i = threadIdx.x; i < a.nbins; i += 256) lhist[i] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < a.nbuf; b += nw) {
+        const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
+        const uint64_t len = a.uniform_len ? a.uniform_len : a.lens[b];
+        const uint64_t word0 = off >> 5;
+        uint64_t start = 0;
+        uint32_t cnt = 0;
+        while (start < len) {
+            const uint64_t lo = start + a.first_off;
+            const uint64_t forced = start + a.max_len - 1;
+            const uint64_t hi = forced < len - 1 ? forced : len - 1;
+            int64_t k = -1;
+            if (lo <= hi) k = find_first(a.bitmap, word0, lo, hi, lane);
+            if (k < 0) k = (int64_t)hi;  // forced cut at max_len, or the tail chunk
+            const uint32_t clen = (uint32_t)(k + 1 - start);
+            if (cnt < a.cap) {
+                if (lane == 0) {
+                    const uint64_t slot = (uint64_t)b * a.cap + cnt;
+                    a.starts[slot] = (uint32_t)start;
+                    a.clens[slot] = clen;
+                    uint32_t bin = sha_blocks(clen) >> a.bin_shift;
+                    bin = bin < a.nbins ? bin : a.nbins - 1;
+                    atomicAdd(&lhist[bin], 1u);
+                }
+            } else if (lane == 0) {
+                atomicOr(a.overflow, 1u);
+            }
+            cnt++;
+            start = (uint64_t)k + 1;
+        }
+        if (lane == 0) a.counts[b] = cnt < a.cap ? cnt : a.cap;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.nbins; i += 256)
+        if (lhist[i]) atomicAdd(&a.hist[i], lhist[i]);
+}
+
+hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
+    uint32_t blocks = (a.nbuf + 3) / 4;
+    // a few buffers per wave so the per-block histogram flush is amortised
+    blocks = (blocks + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(cdc_resolve_kernel, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// 3. prefix: bin cursors (descending bins = longest chunks first) and record bases
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void cdc_prefix_kernel(PrefixArgs a) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x;
+    // bins: cursor[b] = sum_{b' > b} hist[b']
+    part[t] = t < a.nbins ? a.hist[a.nbins - 1 - t] : 0;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    if (t < a.nbins) a.cursor[a.nbins - 1 - t] = part[t] - a.hist[a.nbins - 1 - t];
+    __syncthreads();
+    // record bases: exclusive prefix of counts
+    const uint32_t per = (a.nbuf + 1023) / 1024;
+    const uint32_t b0 = t * per, b1 = (b0 + per < a.nbuf) ? b0 + per : a.nbuf;
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; b++) sum += a.counts[b];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    if (a.rec_base)
+        for (uint32_t b = b0; b < b1; b++) {
+            a.rec_base[b] = run;
+            run += a.counts[b];
+        }
+    if (t == 1023) *a.total = part[1023];
+}
+
+hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// 4. scatter: slot -> position in the longest-first task list (block-aggregated atomics)
+// ------------------------------------------------------------------------------------------
+constexpr int kScatterThreads = 256;
+constexpr int kScatterPer = 8;
+
+__global__ __launch_bounds__(kScatterThreads) void cdc_scatter_kernel(ScatterArgs a) {
+    __shared__ uint32_t lcount[kMaxBins], lbase[kMaxBins];
+    for (uint32_t i = threadIdx.x; i < a.nbins; i += kScatterThreads) lcount[i] = 0;
+    __syncthreads();
+    const uint64_t nslots = (uint64_t)a.nbuf * a.cap;
+    const uint64_t s0 = (uint64_t)blockIdx.x * kScatterThreads * kScatterPer;
+    uint32_t bin[kScatterPer], loc[kScatterPer];
+#pragma unroll
+    for (int k = 0; k < kScatterPer; k++) {
+        const uint64_t slot = s0 + (uint64_t)k * kScatterThreads + threadIdx.x;
+        bin[k] = 0xFFFFFFFFu;
+        if (slot < nslots) {
+            const uint32_t b = (uint32_t)(slot / a.cap);
+            const uint32_t i = (uint32_t)(slot - (uint64_t)b * a.cap);
+            if (i < a.counts[b]) {
+                uint32_t bb = sha_blocks(a.clens[slot]) >> a.bin_shift;
+                bb = bb < a.nbins ? bb : a.nbins - 1;
+                bin[k] = bb;
+                loc[k] = atomicAdd(&lcount[bb], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.nbins; i += kScatterThreads)
+        if (lcount[i]) lbase[i] = atomicAdd(&a.cursor[i], lcount[i]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScatterPer; k++)
+        if (bin[k] != 0xFFFFFFFFu)
+            a.tasks[lbase[bin[k]] + loc[k]] = (uint32_t)(s0 + (uint64_t)k * kScatterThreads + threadIdx.x);
+}
+
+hipError_t launch_scatter(const ScatterArgs& a, hipStream_t s) {
+    const uint64_t nslots = (uint64_t)a.nbuf * a.cap;
+    const uint64_t per_block = (uint64_t)kScatterThreads * kScatterPer;
+    const uint32_t blocks = (uint32_t)((nslots + per_block - 1) / per_block);
+    hipLaunchKernelGGL(cdc_scatter_kernel, dim3(blocks ? blocks : 1), dim3(kScatterThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// 5. per-chunk fingerprint: one lane per chunk (tasks are sorted longest-first so the lanes of
+//    a wave carry near-equal block counts)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+constexpr uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+// SHA-256 compression (FIPS 180-4 6.2.2) on 16 big-endian message words; rotations map to
+// v_alignbit_b32, the Sigma xors and Ch/Maj to v_bitop3_b32, the three-input sums to v_add3_u32.
+__device__ __forceinline__ void sha256_compress(uint32_t (&s)[8], uint32_t (&w)[16]) {
+    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma clang loop unroll(full)
+    for (int i = 0; i < 64; i++) {
+        if (i >= 16 && (i & 15) == 0) {
+            // Message schedule for rounds i..i+15, in place over the 16-word window.  The empty
+            // asm ties the window to the round state so hipcc cannot hoist all of W[16..63]
+            // above the rounds (48 live VGPRs, occupancy 3); it emits no instruction and, since
+            // the old window is dead afterwards, no copies.
+            asm("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
+                "+v"(w[7]), "+v"(w[8]), "+v"(w[9]), "+v"(w[10]), "+v"(w[11]), "+v"(w[12]), "+v"(w[13]),
+                "+v"(w[14]), "+v"(w[15]) : "v"(a));
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+            }
+        }
+        const uint32_t wi = w[i & 15];
+        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+        const uint32_t ch = (e & f) | (~e & g);
+        const uint32_t t1 = h + S1 + ch + kSha256K[i] + wi;
+        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+        const uint32_t mj = maj3(a, b, c);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+    s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+}
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+
+// MD5 compression (RFC 1321 3.4) on 16 little-endian words.
+__device__ __forceinline__ void md5_compress(uint32_t (&s)[4], const uint32_t (&m)[16]) {
+    constexpr uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+    constexpr int R[16] = {7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21};
+    uint32_t a = s[0], b = s[1], c = s[2], d = s[3];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t f;
+        int g;
+        if (i < 16) { f = (b & c) | (~b & d); g = i; }
+        else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) & 15; }
+        else if (i < 48) { f = xor3(b, c, d); g = (3 * i + 5) & 15; }
+        else { f = c ^ (b | ~d); g = (7 * i) & 15; }
+        const uint32_t t = a + f + K[i] + m[g];
+        a = d; d = c; c = b;
+        b = b + rotl(t, R[(i >> 4) * 4 + (i & 3)]);
+    }
+    s[0] += a; s[1] += b; s[2] += c; s[3] += d;
+}
+
+// The chunk's final 1-2 blocks: bytes [0, rem) from `t`, the 0x80 terminator, zero fill and the
+// 64-bit bit length (big-endian for SHA-256, little-endian for MD5).  Only aligned dwords that
+// hold at least one chunk byte are read.
+template <bool SHA>
+__device__ __forceinline__ void tail_words(uint32_t (&m)[16], const uint8_t* t, uint32_t rem) {
+    const uintptr_t ta = reinterpret_cast<uintptr_t>(t);
+    const uint32_t r = (uint32_t)(ta & 3);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(ta - r);
+    const uint32_t nd = (r + rem + 3) >> 2;
+    uint32_t d[17];
+#pragma unroll
+    for (int j = 0; j < 17; j++) d[j] = (uint32_t)j < nd ? q[j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint32_t v = __builtin_amdgcn_alignbyte(d[j + 1], d[j], r);  // little-endian bytes t[4j..4j+3]
+        const int k = (int)rem - 4 * j;
+        if (k <= 0) v = 0;
+        else if (k < 4) v &= (1u << (8 * k)) - 1u;
+        if (k >= 0 && k < 4) v |= 0x80u << (8 * k);
+        m[j] = SHA ? __builtin_bswap32(v) : v;
+    }
+}
+
+template <int ALGO>
+__global__ __launch_bounds__(256) void chunk_hash_kernel(HashArgs a) {
+    constexpr bool SHA = ALGO != 2;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= *a.total) return;
+    const uint32_t slot = a.tasks[i];
+    const uint32_t b = slot / a.cap;
+    const uint32_t k = slot - b * a.cap;
+    const uint64_t boff = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
+    const uint32_t cs = a.starts[slot];
+    const uint32_t len = a.clens[slot];
+    const uint8_t* p = a.data + boff + cs;
+    const uint32_t nfull = len >> 6;           // whole 64-byte data blocks
+    const uint32_t nblocks = (len + 8) / 64 + 1;  // + terminator/length block(s)
+    const uint64_t bits = (uint64_t)len * 8;
+    uint32_t s[8];
+    if constexpr (SHA) {
+        s[0] = 0x6a09e667; s[1] = 0xbb67ae85; s[2] = 0x3c6ef372; s[3] = 0xa54ff53a;
+        s[4] = 0x510e527f; s[5] = 0x9b05688c; s[6] = 0x1f83d9ab; s[7] = 0x5be0cd19;
+    } else {
+        s[0] = 0x67452301; s[1] = 0xefcdab89; s[2] = 0x98badcfe; s[3] = 0x10325476;
+        s[4] = s[5] = s[6] = s[7] = 0;
+    }
+    // One compression per block; lanes of a wave hold chunks of near-equal block count
+    // (longest-first binning), so the data/tail branch below is wave-uniform almost always.
+    for (uint32_t blk = 0; blk < nblocks; blk++) {
+        uint32_t w[16];
+        if (blk < nfull) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint4 v;
+                __builtin_memcpy(&v, p + 64 * blk + 16 * q, 16);  // unaligned global_load_dwordx4
+                w[4 * q] = SHA ? __builtin_bswap32(v.x) : v.x;
+                w[4 * q + 1] = SHA ? __builtin_bswap32(v.y) : v.y;
+                w[4 * q + 2] = SHA ? __builtin_bswap32(v.z) : v.z;
+                w[4 * q + 3] = SHA ? __builtin_bswap32(v.w) : v.w;
+            }
+        } else {
+            if (blk == nfull) {
+                tail_words<SHA>(w, p + 64 * nfull, len & 63);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; j++) w[j] = 0;
+            }
+            if (blk == nblocks - 1) {
+                w[14] = SHA ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+                w[15] = SHA ? (uint32_t)bits : (uint32_t)(bits >> 32);
+            }
+        }
+        if constexpr (SHA) {
+            sha256_compress(s, w);
+        } else {
+            uint32_t m4[4] = {s[0], s[1], s[2], s[3]};
+            md5_compress(m4, w);
+            s[0] = m4[0]; s[1] = m4[1]; s[2] = m4[2]; s[3] = m4[3];
+        }
+    }
+    uint32_t dig[8];
+    if constexpr (SHA) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) dig[j] = __builtin_bswap32(s[j]);
+        if constexpr (ALGO == 1) dig[5] = dig[6] = dig[7] = 0;  // VARIABLE_SHA256_160: first 20 bytes
+    } else {
+        dig[0] = s[0]; dig[1] = s[1]; dig[2] = s[2]; dig[3] = s[3];
+        dig[4] = dig[5] = dig[6] = dig[7] = 0;
+    }
+    uint4* out = reinterpret_cast<uint4*>(a.digests + (uint64_t)slot * 32);
+    const uint4 d0 = make_uint4(dig[0], dig[1], dig[2], dig[3]);
+    const uint4 d1 = make_uint4(dig[4], dig[5], dig[6], dig[7]);
+    out[0] = d0;
+    out[1] = d1;
+    if (a.records) {
+        const uint64_t r = (uint64_t)a.rec_base[b] + k;
+        if (r < a.records_cap) {
+            uint4* rec = reinterpret_cast<uint4*>(a.records + r * kRecordBytes);
+            const uint64_t id = a.buffer_id_base + b;
+            rec[0] = d0;
+            rec[1] = d1;
+            rec[2] = make_uint4((uint32_t)id, (uint32_t)(id >> 32), cs, len);
+        }
+    }
+}
+
+hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, hipStream_t s) {
+    const uint32_t blocks = (uint32_t)((max_tasks + 255) / 256);
+    if (blocks == 0) return hipSuccess;
+    switch (a.algo) {
+    case 0: hipLaunchKernelGGL((chunk_hash_kernel<0>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((chunk_hash_kernel<1>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((chunk_hash_kernel<2>), dim3(blocks), dim3(256), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// synthetic input: byte o of stream s = byte (o%8) of splitmix64(key + o/8)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(uint8_t* out, uint64_t n, uint64_t key, uint64_t offset) {
+    const uint64_t nw = ((offset + n + 7) >> 3) - (offset >> 3);
+    const bool fast = ((offset & 7) == 0) && ((reinterpret_cast<uintptr_t>(out) & 7) == 0);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t wi = (offset >> 3) + i;
+        const uint64_t v = splitmix64(key + wi);
+        const uint64_t b0 = wi * 8;  // stream byte offset of this word
+        if (fast && b0 + 8 <= offset + n) {
+            *reinterpret_cast<uint64_t*>(out + (b0 - offset)) = v;
+        } else {
+            for (int k = 0; k < 8; k++) {
+                const uint64_t o = b0 + k;
+                if (o >= offset && o < offset + n) out[o - offset] = (uint8_t)(v >> (8 * k));
+            }
+        }
+    }
+}
+
+hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
+                        hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t key = splitmix64_host(seed ^ (stream_id * 0xD1B54A32D192ED03ull));
+    const uint64_t nw = ((offset + n + 7) >> 3) - (offset >> 3);
+    uint64_t blocks = (nw + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(synth_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, out, n, key, offset);
+    return hipGetLastError();
+}
+
+}  // namespace sdfs
