@@ -57,12 +57,33 @@ __device__ __forceinline__ void push_step(uint32_t& lo, uint32_t& hi, uint32_t d
     hi = nhi ^ pv.y;
 }
 
+// Shift the candidate flag of the current position into `bits` (first position ends in the MSB,
+// bit-reversed once per 32 positions).  Written as one v_and/v_cmp/v_addc sequence: in plain C
+// hipcc reassociates the 32 per-byte tests of a word into an OR tree at the end of the word,
+// keeping all 32 fingerprints live (scratch spills on every byte).
 template <bool PRED64>
-__device__ __forceinline__ uint32_t cand_bit(uint32_t lo, uint32_t hi, const ScanArgs& a) {
-    if constexpr (PRED64)
-        return ((lo & a.mask_lo) == a.val_lo) & ((hi & a.mask_hi) == a.val_hi);
-    else
-        return (lo & a.mask_lo) == a.val_lo;
+__device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t hi, const ScanArgs& a) {
+    uint32_t t;
+    if constexpr (PRED64) {
+        uint32_t t2;
+        asm("v_and_b32 %1, %4, %3\n\t"
+            "v_xor_b32 %1, %5, %1\n\t"
+            "v_and_b32 %2, %7, %6\n\t"
+            "v_xor_b32 %2, %8, %2\n\t"
+            "v_or_b32 %1, %1, %2\n\t"
+            "v_cmp_eq_u32 vcc, 0, %1\n\t"
+            "v_addc_co_u32 %0, vcc, %0, %0, vcc"
+            : "+v"(bits), "=&v"(t), "=&v"(t2)
+            : "v"(lo), "s"(a.mask_lo), "s"(a.val_lo), "v"(hi), "s"(a.mask_hi), "s"(a.val_hi)
+            : "vcc");
+    } else {
+        asm("v_and_b32 %1, %3, %2\n\t"
+            "v_cmp_eq_u32 vcc, %4, %1\n\t"
+            "v_addc_co_u32 %0, vcc, %0, %0, vcc"
+            : "+v"(bits), "=&v"(t)
+            : "v"(lo), "s"(a.mask_lo), "s"(a.val_lo)
+            : "vcc");
+    }
 }
 
 // Byte o of the current 64-byte block, with the byte that leaves the window at o - W
@@ -75,7 +96,7 @@ __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& 
     constexpr int OI = OLD >= 0 ? OLD : OLD + 64;
     const uint32_t odw = OLD >= 0 ? cur[OI >> 2] : prev[OI >> 2];
     roll_step<(O & 3), (OI & 3)>(lo, hi, cur[O >> 2], odw, c8, push_base, a.jshift, tab);
-    bits |= cand_bit<PRED64>(lo, hi, a) << (O & 31);
+    cand_shift<PRED64>(bits, lo, hi, a);
 }
 
 #ifndef SDFS_SCAN_SCHED_GROUP
@@ -219,13 +240,13 @@ __global__ __launch_bounds__(kScanThreads) void cdc_scan_kernel(ScanArgs a) {
             bytes_from<W, PRED64, 0, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
             uint32_t w0[NCH];
 #pragma unroll
-            for (int c = 0; c < NCH; c++) { w0[c] = bits[c]; bits[c] = 0; }
+            for (int c = 0; c < NCH; c++) { w0[c] = __builtin_bitreverse32(bits[c]); bits[c] = 0; }
             bytes_from_hi<W, PRED64, 32, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 if (blk < nblk[c]) {
                     const uint64_t pos = start[c] + 64ull * blk;
-                    *reinterpret_cast<uint2*>(a.bitmap + (pos >> 5)) = make_uint2(w0[c], bits[c]);
+                    *reinterpret_cast<uint2*>(a.bitmap + (pos >> 5)) = make_uint2(w0[c], __builtin_bitreverse32(bits[c]));
                 }
 #pragma unroll
                 for (int i = 0; i < 16; i++) prev[c][i] = cur[c][i];

@@ -212,7 +212,7 @@ def test_device_b1_full_size_properties():
     # dense record table == per-buffer slots, in (buffer, chunk) order
     rec = batch.record_table().cpu().numpy()
     assert rec.shape[0] == total
-    base = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    base = np.concatenate([[0], np.cumsum(counts.astype(np.int64))[:-1]]).astype(np.int64)
     for b in sample:
         for i in range(counts[b]):
             r = rec[base[b] + i]
