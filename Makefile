@@ -6,8 +6,17 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 CSRC := sdfs_amd/csrc
 LIB := sdfs_amd/libsdfs_cdc.so
 OBJS := build/cdc_kernels.o build/cdc_engine.o
+SWEEP_LIB := sdfs_amd/libsdfs_cdc_sweep.so
 
 all: $(LIB) oracle
+
+# kernel-variant sweep build (scripts/sweep_scan.py); not used by the product path
+sweep: $(SWEEP_LIB)
+build/sweep_kernels.o: $(CSRC)/cdc_kernels.hip $(CSRC)/cdc_internal.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DSDFS_SCAN_SWEEP -c $< -o $@
+$(SWEEP_LIB): build/sweep_kernels.o build/cdc_engine.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 build/%.o: $(CSRC)/%.hip $(CSRC)/cdc_internal.h include/sdfs_cdc.h
 	@mkdir -p build
@@ -23,4 +32,4 @@ clean:
 	rm -rf build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean sweep

@@ -11,7 +11,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsdfs_cdc.so")
+# SDFS_CDC_LIB selects an alternative in-tree build (kernel-variant sweeps, scripts/sweep_scan.py)
+LIB_PATH = os.environ.get("SDFS_CDC_LIB") or os.path.join(HERE, "libsdfs_cdc.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "sdfs_cdc.h")
 
 OK, EINVAL, ECAP, EHIP, ENOMEM, ENODEV = 0, -1, -2, -3, -4, -5

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -49,8 +50,8 @@ uint64_t mulx_mod(uint64_t v, uint64_t poly, int d) {
 }
 
 // Rolling-hash tables (same definition as the jar's precompute), laid out as the
-// scan kernel's LDS image with kTabCopies lane-private copies.
-std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window) {
+// scan kernel's LDS image with `copies` lane-private copies (cdc_internal.h).
+std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window, int copies) {
     const int d = poly_degree(poly);
     std::vector<uint64_t> push(256), pop(256);
     for (uint64_t i = 0; i < 256; i++) {
@@ -61,11 +62,12 @@ std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window) {
         for (uint32_t k = 0; k < 8 * window; k++) q = mulx_mod(q, poly, d);
         pop[i] = q;
     }
-    std::vector<uint8_t> img(kTabBytes);
-    for (int e = 0; e < 256; e++)
-        for (int c = 0; c < kTabCopies; c++) {
+    std::vector<uint8_t> img(scan_lds_bytes(copies));
+    const uint32_t push_off = copies == 32 ? 0x10000u : 0x80u;
+    for (uint32_t e = 0; e < 256; e++)
+        for (uint32_t c = 0; c < (uint32_t)copies; c++) {
             memcpy(&img[(e << 8) | (c << 3)], &pop[e], 8);
-            memcpy(&img[kPushBase | (e << 8) | (c << 3)], &push[e], 8);
+            memcpy(&img[push_off | (e << 8) | (c << 3)], &push[e], 8);
         }
     return img;
 }
@@ -101,7 +103,9 @@ struct sdfs_cdc_engine {
     sdfs_cdc_params prm{};
     int degree = 0;
     int num_cus = 256;
-    uint32_t seg_len = 2048;
+    uint32_t seg_len = 4096;  // bytes of one buffer per lane (multiple of the variant's block)
+    int scan_variant = 0;
+    ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
     uint32_t digest_len = 32;
@@ -227,12 +231,12 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
         seg_bound = data_bytes / e->seg_len + nbuf;
     }
     if (timing) HIP_TRY(hipEventRecord(e->ev[1], s));
-    const uint64_t per_block = (uint64_t)kScanThreads * kScanChains;
+    const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
     uint64_t grid = (seg_bound + per_block - 1) / per_block;
-    grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus);
+    grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus * e->scan_info.wg_per_cu);
     grid = std::max<uint64_t>(grid, 1);
     const bool pred64 = (e->prm.pred_mask >> 32) != 0;
-    HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, (int)grid, s));
+    HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, s));
     if (timing) HIP_TRY(hipEventRecord(e->ev[2], s));
 
     ResolveArgs ra{};
@@ -439,9 +443,17 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
         delete e;
         return fail(SDFS_CDC_EHIP, "hipStreamCreate failed");
     }
-    std::vector<uint8_t> img = build_table_image(p->poly, p->window);
-    if (e->tab_image.ensure(kTabBytes) != hipSuccess ||
-        hipMemcpy(e->tab_image.p, img.data(), kTabBytes, hipMemcpyHostToDevice) != hipSuccess) {
+    // tuning overrides for experiments (DESIGN.md "Scan variants"); production uses variant 0
+    if (const char* v = getenv("SDFS_SCAN_VARIANT")) e->scan_variant = atoi(v);
+    if (const char* v = getenv("SDFS_SEG_LEN")) e->seg_len = (uint32_t)atoi(v);
+    e->scan_info = scan_variant_info(e->scan_variant);
+    if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0) {
+        sdfs_cdc_destroy(e);
+        return fail(SDFS_CDC_EINVAL, "bad scan variant/segment length");
+    }
+    std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies);
+    if (e->tab_image.ensure(img.size()) != hipSuccess ||
+        hipMemcpy(e->tab_image.p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
         sdfs_cdc_destroy(e);
         return fail(SDFS_CDC_ENOMEM, "table upload failed");
     }

@@ -6,16 +6,24 @@
 
 namespace sdfs {
 
-// LDS image of the rolling-hash tables (DESIGN.md "Rabin scan"): 32 lane-private copies so that
-// every ds_read_b64 of a 32-lane group hits 32 distinct bank pairs (conflict-free for random
-// indices).  pop table at [0, 64K): entry o, copy c at byte (o << 8) | (c << 3);
-// push table at [64K, 128K): entry j, copy c at 0x10000 | (j << 8) | (c << 3).
-constexpr int kTabCopies = 32;
-constexpr int kTabBytes = 2 * 256 * kTabCopies * 8;  // 131072
-constexpr int kPushBase = 0x10000;
+// LDS image of the rolling-hash tables (DESIGN.md "Rabin scan"): C lane-private copies of each
+// 256 x 8-byte table; lane l reads copy (l mod C), so with C = 32 every ds_read_b64 of a 32-lane
+// group hits 32 distinct bank pairs (conflict-free for random indices), with C = 16 two lanes
+// share a bank pair (2-way).  Entry e of the pop table, copy c: byte (e << 8) | (c << 3).
+// Push table: C = 32 -> 0x10000 | (e << 8) | (c << 3) (two 64 KiB tables);
+//             C = 16 -> (e << 8) | 0x80 | (c << 3) (interleaved with pop in 256-byte rows).
+constexpr int scan_lds_bytes(int copies) { return 2 * 256 * copies * 8; }
 
-constexpr int kScanThreads = 1024;  // one workgroup per CU (128 KiB LDS)
-constexpr int kScanChains = 2;      // independent segments per lane (ILP across the LDS latency)
+constexpr int kScanThreads = 1024;
+
+struct ScanVariantInfo {
+    int copies;      // table copies (image layout)
+    int chains;      // segments per lane
+    int lds_bytes;   // LDS image size
+    int wg_per_cu;   // resident workgroups per CU the variant is built for
+    int blk;         // bytes per lane per iteration (segment length must be a multiple)
+};
+ScanVariantInfo scan_variant_info(int variant);
 
 constexpr int kMaxBins = 512;  // SHA work binning by block count (DESIGN.md "Load balance")
 constexpr int kRecordBytes = 48;
@@ -32,7 +40,7 @@ struct ScanArgs {
     uint32_t seg_len;            // bytes per segment, multiple of 64
     uint32_t jshift;             // deg(P) - 40 : bit offset of the push index inside the hi word
     uint32_t mask_lo, mask_hi, val_lo, val_hi;
-    const uint8_t* tab_image;    // kTabBytes, global copy of the LDS image
+    const uint8_t* tab_image;    // global copy of the LDS image (scan_lds_bytes(copies))
 };
 
 struct ResolveArgs {
@@ -101,7 +109,7 @@ inline uint64_t splitmix64_host(uint64_t x) {
 // kernel launchers (cdc_kernels.hip); all asynchronous on `stream`
 hipError_t launch_seg_prefix(const uint32_t* lens, uint32_t nbuf, uint32_t seg_len, uint64_t* seg_prefix,
                              hipStream_t stream);
-hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int grid, hipStream_t stream);
+hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t stream);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);

@@ -31,14 +31,17 @@ __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
 // pushByte/popByte pair:
 //   j = (fp >> (d-8)) & 0xFF;  fp = ((fp << 8) | b) ^ push[j];  fp ^= pop[o]
 // push[j] carries j*x^d, which cancels the 8 bits shifted above deg-1.
-template <int P, int Q>
+// Ablation bits (scan sweeps only; production ABL = 0): 1 = no pop LDS read, 2 = no push LDS
+// read, 4 = no candidate test, 8 = no global loads.  The skipped values are replaced by register
+// values that keep every remaining instruction live.
+template <int P, int Q, int ABL = 0>
 __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
                                           uint32_t push_base, uint32_t jshift, const uint8_t* tab) {
     const uint32_t j = __builtin_amdgcn_ubfe(hi, jshift, 8);
     const uint32_t pa = (j << 8) | push_base;                                          // push[j], lane copy
     const uint32_t qa = __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + Q) << 8));  // (o << 8) | c8
-    const uint2 pv = *reinterpret_cast<const uint2*>(tab + pa);
-    const uint2 qv = *reinterpret_cast<const uint2*>(tab + qa);
+    const uint2 pv = (ABL & 2) ? make_uint2(pa, pa >> 3) : *reinterpret_cast<const uint2*>(tab + pa);
+    const uint2 qv = (ABL & 1) ? make_uint2(qa, qa >> 3) : *reinterpret_cast<const uint2*>(tab + qa);
     const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);             // (fp << 8) >> 32
     const uint32_t nlo = __builtin_amdgcn_perm(lo, dw, 0x06050400u | P);     // (lo << 8) | b
     lo = xor3(nlo, pv.x, qv.x);
@@ -86,17 +89,20 @@ __device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t
     }
 }
 
-// Byte o of the current 64-byte block, with the byte that leaves the window at o - W
-// (in this block when o >= W, otherwise in the previous block).
-template <int W, bool PRED64, int O>
-__device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& bits, const uint32_t (&cur)[16],
+// Byte O of the current block (BLKW dwords), with the byte that leaves the window at O - W: in
+// this block when O >= W, otherwise in `prev` (the previous block's last 64 bytes).
+template <int W, bool PRED64, int O, int ABL, int BLKW>
+__device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& bits, const uint32_t (&cur)[BLKW],
                                           const uint32_t (&prev)[16], uint32_t c8, uint32_t push_base,
                                           const uint8_t* tab, const ScanArgs& a) {
     constexpr int OLD = O - W;  // may be negative -> previous block
     constexpr int OI = OLD >= 0 ? OLD : OLD + 64;
     const uint32_t odw = OLD >= 0 ? cur[OI >> 2] : prev[OI >> 2];
-    roll_step<(O & 3), (OI & 3)>(lo, hi, cur[O >> 2], odw, c8, push_base, a.jshift, tab);
-    cand_shift<PRED64>(bits, lo, hi, a);
+    roll_step<(O & 3), (OI & 3), ABL>(lo, hi, cur[O >> 2], odw, c8, push_base, a.jshift, tab);
+    if constexpr (ABL & 4)
+        bits ^= lo;
+    else
+        cand_shift<PRED64>(bits, lo, hi, a);
 }
 
 #ifndef SDFS_SCAN_SCHED_GROUP
@@ -104,29 +110,20 @@ __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& 
 #endif
 constexpr int kSchedGroup = SDFS_SCAN_SCHED_GROUP;  // bytes per scheduling region
 
-template <int W, bool PRED64, int O, int NCH>
-__device__ __forceinline__ void bytes_from(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
-                                           const uint32_t (&cur)[NCH][16], const uint32_t (&prev)[NCH][16],
+// Positions O .. O0+31 of one candidate word, all chains interleaved (independent rolling chains
+// give the ILP that hides the LDS latency of the push lookups).
+template <int W, bool PRED64, int O0, int O, int NCH, int ABL, int BLKW>
+__device__ __forceinline__ void word_steps(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
+                                           const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
                                            uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
-    if constexpr (O < 32) {
+    if constexpr (O < O0 + 32) {
 #pragma unroll
-        for (int c = 0; c < NCH; c++) byte_step<W, PRED64, O>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
+        for (int c = 0; c < NCH; c++)
+            byte_step<W, PRED64, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
         // keep the scheduler from hoisting every (chain-independent) pop read of the block
         // ahead of the rolling chain: that costs ~2 VGPRs per byte and spills.
         if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) __builtin_amdgcn_sched_barrier(0);
-        bytes_from<W, PRED64, O + 1, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
-    }
-}
-template <int W, bool PRED64, int O, int NCH>
-__device__ __forceinline__ void bytes_from_hi(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
-                                              const uint32_t (&cur)[NCH][16], const uint32_t (&prev)[NCH][16],
-                                              uint32_t c8, uint32_t push_base, const uint8_t* tab,
-                                              const ScanArgs& a) {
-    if constexpr (O < 64) {
-#pragma unroll
-        for (int c = 0; c < NCH; c++) byte_step<W, PRED64, O>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
-        if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) __builtin_amdgcn_sched_barrier(0);
-        bytes_from_hi<W, PRED64, O + 1, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+        word_steps<W, PRED64, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
     }
 }
 
@@ -139,38 +136,74 @@ __device__ __forceinline__ void warm_from(uint32_t& lo, uint32_t& hi, const uint
     }
 }
 
-// Load the 64-byte block at byte address `addr` if it is readable up to `lim`; dwords that hold
-// no byte below `lim` read as zero (only the buffer's last block takes the guarded path).
-__device__ __forceinline__ void load_block(uint32_t (&d)[16], const uint8_t* data, uint64_t addr, uint64_t lim) {
-    const bool full = addr + 64 <= lim;
+// Load N dwords at byte address `addr` if readable up to `lim`; dwords that hold no byte below
+// `lim` read as zero (only a buffer's last block takes the guarded path).
+template <int N>
+__device__ __forceinline__ void load_block(uint32_t (&d)[N], const uint8_t* data, uint64_t addr, uint64_t lim) {
+    const bool full = addr + 4 * N <= lim;
     if (__all(full)) {
         const uint4* p = reinterpret_cast<const uint4*>(data + addr);
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < N / 4; i++) {
             const uint4 v = p[i];
             d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
         }
     } else {
         const uint32_t* p = reinterpret_cast<const uint32_t*>(data + addr);
 #pragma unroll
-        for (int i = 0; i < 16; i++) d[i] = (addr + 4 * i < lim) ? p[i] : 0u;
+        for (int i = 0; i < N; i++) d[i] = (addr + 4 * i < lim) ? p[i] : 0u;
     }
 }
 
-template <int W, bool PRED64>
-__global__ __launch_bounds__(kScanThreads) void cdc_scan_kernel(ScanArgs a) {
-    constexpr int NCH = kScanChains;
-    __shared__ __attribute__((aligned(16))) uint8_t tab[kTabBytes];
+// All candidate words of one block: word WI covers positions 32*WI .. 32*WI+31.
+template <int W, bool PRED64, int WI, int NW, int NCH, int ABL, int BLKW>
+__device__ __forceinline__ void block_words(uint32_t (&words)[NCH][NW], uint32_t (&lo)[NCH], uint32_t (&hi)[NCH],
+                                            const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
+                                            uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
+    if constexpr (WI < NW) {
+        uint32_t bits[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; c++) bits[c] = 0;
+        word_steps<W, PRED64, 32 * WI, 32 * WI, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+#pragma unroll
+        for (int c = 0; c < NCH; c++) words[c][WI] = __builtin_bitreverse32(bits[c]);
+        block_words<W, PRED64, WI + 1, NW, NCH, ABL, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+    }
+}
+
+// Scan variants (DESIGN.md "Rabin scan"): C lane-private table copies (32: conflict-free,
+// 128 KiB, one 1024-thread workgroup per CU; 16: 2-way, 64 KiB, two workgroups per CU), NCH
+// independent segments per lane, BLK bytes per lane per iteration (128 = one whole cache line
+// per lane per load, so no line is fetched twice), PF = prefetch the next block.
+template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64>
+struct ScanCfg {
+    static constexpr int kAbl = ABL;
+    static constexpr int kCopies = C;
+    static constexpr int kChains = NCH;
+    static constexpr bool kPrefetch = PF;
+    static constexpr int kWavesPerSimd = WPS;  // __launch_bounds__ occupancy request
+    static constexpr int kLds = scan_lds_bytes(C);
+    static constexpr uint32_t kPushOff = C == 32 ? 0x10000u : 0x80u;
+    static constexpr int kBlk = BLK;
+};
+
+template <int W, bool PRED64, class CFG>
+__global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
+    constexpr int NCH = CFG::kChains;
+    constexpr int C = CFG::kCopies;
+    constexpr int BLK = CFG::kBlk;
+    constexpr int BLKW = BLK / 4;
+    __shared__ __attribute__((aligned(16))) uint8_t tab[CFG::kLds];
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.tab_image);
         uint4* dst = reinterpret_cast<uint4*>(tab);
-        for (int i = threadIdx.x; i < kTabBytes / 16; i += kScanThreads) dst[i] = src[i];
+        for (int i = threadIdx.x; i < CFG::kLds / 16; i += kScanThreads) dst[i] = src[i];
     }
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c8 = (lane & 31) << 3;
-    const uint32_t push_base = kPushBase | c8;
+    const uint32_t c8 = (lane & (C - 1)) << 3;
+    const uint32_t push_base = CFG::kPushOff | c8;
     const uint64_t total = a.uniform_len ? a.total_segs : a.seg_prefix[a.nbuf];
     const uint64_t per_iter = (uint64_t)kScanThreads * NCH;
 
@@ -186,11 +219,11 @@ __global__ __launch_bounds__(kScanThreads) void cdc_scan_kernel(ScanArgs a) {
             nblk[c] = 0;
             first[c] = true;
             if (seg < total) {
-                uint64_t bstart, blen, s;
+                uint64_t bstart, blen, sidx;
                 if (a.uniform_len) {
                     const uint64_t spb = (a.uniform_len + a.seg_len - 1) / a.seg_len;
                     const uint64_t b = seg / spb;
-                    s = seg - b * spb;
+                    sidx = seg - b * spb;
                     bstart = b * a.uniform_len;
                     blen = a.uniform_len;
                 } else {
@@ -199,59 +232,139 @@ __global__ __launch_bounds__(kScanThreads) void cdc_scan_kernel(ScanArgs a) {
                         const uint32_t mid = (lo_b + hi_b) >> 1;
                         if (a.seg_prefix[mid] <= seg) lo_b = mid; else hi_b = mid;
                     }
-                    s = seg - a.seg_prefix[lo_b];
+                    sidx = seg - a.seg_prefix[lo_b];
                     bstart = a.offs[lo_b];
                     blen = a.lens[lo_b];
                 }
-                start[c] = bstart + s * a.seg_len;
+                start[c] = bstart + sidx * a.seg_len;
                 const uint64_t bend = bstart + blen;
                 end[c] = start[c] + a.seg_len < bend ? start[c] + a.seg_len : bend;
-                nblk[c] = (uint32_t)((end[c] - start[c] + 63) >> 6);
-                // window warm-up needs the previous block unless this is the buffer's first segment
+                nblk[c] = (uint32_t)((end[c] - start[c] + BLK - 1) / BLK);
+                // window warm-up reads the previous 64 bytes unless this is the buffer's first segment
                 first[c] = start[c] == bstart;
             }
             maxblk = nblk[c] > maxblk ? nblk[c] : maxblk;
         }
 
         uint32_t lo[NCH], hi[NCH];
-        uint32_t prev[NCH][16], cur[NCH][16];
+        uint32_t prev[NCH][16], cur[NCH][BLKW];
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             if (nblk[c] != 0 && !first[c]) {
-                load_block(prev[c], a.data, start[c] - 64, start[c]);
+                load_block<16>(prev[c], a.data, start[c] - 64, start[c]);
             } else {
 #pragma unroll
                 for (int i = 0; i < 16; i++) prev[c][i] = 0;  // bytes before the buffer are empty
             }
             lo[c] = hi[c] = 0;
             warm_from<W, 64 - W>(lo[c], hi[c], prev[c], push_base, a.jshift, tab);
+            if constexpr (CFG::kPrefetch) {
+                const bool act = nblk[c] != 0;
+                load_block<BLKW>(cur[c], a.data, act ? start[c] : 0, act ? end[c] : 0);
+            }
         }
 
         for (uint32_t blk = 0; blk < maxblk; blk++) {
+            uint32_t nxt[NCH][CFG::kPrefetch ? BLKW : 1];
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
-                const bool act = blk < nblk[c];
-                const uint64_t addr = act ? start[c] + 64ull * blk : 0;
-                load_block(cur[c], a.data, addr, act ? end[c] : 0);
+                if constexpr (CFG::kPrefetch) {
+                    const bool act = blk + 1 < nblk[c];
+                    load_block<BLKW>(nxt[c], a.data, act ? start[c] + (uint64_t)BLK * (blk + 1) : 0, act ? end[c] : 0);
+                } else if constexpr (CFG::kAbl & 8) {
+#pragma unroll
+                    for (int i = 0; i < BLKW; i++) cur[c][i] = prev[c][i & 15] * 0x9E3779B1u + blk;
+                } else {
+                    const bool act = blk < nblk[c];
+                    load_block<BLKW>(cur[c], a.data, act ? start[c] + (uint64_t)BLK * blk : 0, act ? end[c] : 0);
+                }
             }
-            uint32_t bits[NCH];
-#pragma unroll
-            for (int c = 0; c < NCH; c++) bits[c] = 0;
-            bytes_from<W, PRED64, 0, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
-            uint32_t w0[NCH];
-#pragma unroll
-            for (int c = 0; c < NCH; c++) { w0[c] = __builtin_bitreverse32(bits[c]); bits[c] = 0; }
-            bytes_from_hi<W, PRED64, 32, NCH>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+            uint32_t words[NCH][BLK / 32];
+            block_words<W, PRED64, 0, BLK / 32, NCH, CFG::kAbl, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 if (blk < nblk[c]) {
-                    const uint64_t pos = start[c] + 64ull * blk;
-                    *reinterpret_cast<uint2*>(a.bitmap + (pos >> 5)) = make_uint2(w0[c], __builtin_bitreverse32(bits[c]));
+                    const uint64_t pos = start[c] + (uint64_t)BLK * blk;
+                    uint32_t* bm = a.bitmap + (pos >> 5);
+                    if (pos + BLK <= end[c]) {
+                        if constexpr (BLK >= 128) {
+#pragma unroll
+                            for (int w = 0; w < BLK / 32; w += 4)
+                                *reinterpret_cast<uint4*>(bm + w) =
+                                    make_uint4(words[c][w], words[c][w + 1], words[c][w + 2], words[c][w + 3]);
+                        } else {
+                            *reinterpret_cast<uint2*>(bm) = make_uint2(words[c][0], words[c][1]);
+                        }
+                    } else {
+                        // buffer tail: words past the buffer end may belong to the next buffer
+#pragma unroll
+                        for (int w = 0; w < BLK / 32; w++)
+                            if (pos + 32 * w < end[c]) bm[w] = words[c][w];
+                    }
                 }
 #pragma unroll
-                for (int i = 0; i < 16; i++) prev[c][i] = cur[c][i];
+                for (int i = 0; i < 16; i++) prev[c][i] = cur[c][BLKW - 16 + i];
+                if constexpr (CFG::kPrefetch) {
+#pragma unroll
+                    for (int i = 0; i < BLKW; i++) cur[c][i] = nxt[c][i];
+                }
             }
         }
+    }
+}
+
+// variant table (id 0 = production default; the others are built only for sweeps).  Production:
+// 32 conflict-free table copies, one segment per lane, one whole 128-byte line per lane per load
+// (measured 1.56 ms / 4 GiB on MI355X vs 2.6 ms with 64-byte loads, DESIGN.md "Scan variants").
+using ScanV0 = ScanCfg<32, 1, false, 4, 0, 128>;
+using ScanV16 = ScanCfg<32, 2, false, 4>;  // round-1 first version: 64-byte loads, 2 chains
+using ScanV1 = ScanCfg<32, 2, true, 4>;
+using ScanV2 = ScanCfg<32, 1, true, 4>;
+using ScanV3 = ScanCfg<16, 1, true, 8>;
+using ScanV4 = ScanCfg<16, 1, false, 8>;
+using ScanV5 = ScanCfg<16, 2, false, 4>;
+using ScanV6 = ScanCfg<32, 2, false, 4, 0, 128>;
+using ScanV7 = ScanCfg<32, 1, false, 4, 0, 128>;
+using ScanV8 = ScanCfg<16, 1, false, 8, 0, 128>;
+using ScanV9 = ScanCfg<32, 1, true, 4, 0, 128>;
+using ScanV10 = ScanCfg<32, 1, false, 4, 0, 256>;
+using ScanV15 = ScanCfg<32, 2, false, 4, 0, 256>;
+using ScanA1 = ScanCfg<32, 2, false, 4, 1>;   // no pop read
+using ScanA2 = ScanCfg<32, 2, false, 4, 2>;   // no push read
+using ScanA3 = ScanCfg<32, 2, false, 4, 3>;   // no LDS at all
+using ScanA4 = ScanCfg<32, 2, false, 4, 4>;   // no candidate test
+using ScanA8 = ScanCfg<32, 2, false, 4, 8>;   // no global loads
+using ScanA15 = ScanCfg<32, 2, false, 4, 15>; // only the rolling arithmetic
+
+template <class CFG>
+constexpr ScanVariantInfo info_of() {
+    return {CFG::kCopies, CFG::kChains, CFG::kLds, CFG::kWavesPerSimd / 4, CFG::kBlk};
+}
+
+ScanVariantInfo scan_variant_info(int v) {
+    switch (v) {
+    case 0: return info_of<ScanV0>();
+#ifdef SDFS_SCAN_SWEEP
+    case 1: return info_of<ScanV1>();
+    case 2: return info_of<ScanV2>();
+    case 3: return info_of<ScanV3>();
+    case 4: return info_of<ScanV4>();
+    case 5: return info_of<ScanV5>();
+    case 6: return info_of<ScanV6>();
+    case 7: return info_of<ScanV7>();
+    case 8: return info_of<ScanV8>();
+    case 9: return info_of<ScanV9>();
+    case 10: return info_of<ScanV10>();
+    case 15: return info_of<ScanV15>();
+    case 16: return info_of<ScanV16>();
+    case 11: return info_of<ScanA1>();
+    case 12: return info_of<ScanA2>();
+    case 13: return info_of<ScanA3>();
+    case 14: return info_of<ScanA4>();
+    case 18: return info_of<ScanA8>();
+    case 25: return info_of<ScanA15>();
+#endif
+    default: return {0, 0, 0, 0, 0};
     }
 }
 
@@ -259,21 +372,38 @@ bool scan_window_supported(int window) {
     return window == 16 || window == 32 || window == 48 || window == 64;
 }
 
-template <int W>
-static hipError_t launch_scan_w(const ScanArgs& a, bool pred64, int grid, hipStream_t s) {
+template <int W, class CFG>
+static hipError_t launch_scan_wc(const ScanArgs& a, bool pred64, int grid, hipStream_t s) {
     if (pred64)
-        hipLaunchKernelGGL((cdc_scan_kernel<W, true>), dim3(grid), dim3(kScanThreads), 0, s, a);
+        hipLaunchKernelGGL((cdc_scan_kernel<W, true, CFG>), dim3(grid), dim3(kScanThreads), 0, s, a);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<W, false>), dim3(grid), dim3(kScanThreads), 0, s, a);
+        hipLaunchKernelGGL((cdc_scan_kernel<W, false, CFG>), dim3(grid), dim3(kScanThreads), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int grid, hipStream_t s) {
+template <class CFG>
+static hipError_t launch_scan_c(const ScanArgs& a, int window, bool pred64, int grid, hipStream_t s) {
     switch (window) {
-    case 16: return launch_scan_w<16>(a, pred64, grid, s);
-    case 32: return launch_scan_w<32>(a, pred64, grid, s);
-    case 48: return launch_scan_w<48>(a, pred64, grid, s);
-    case 64: return launch_scan_w<64>(a, pred64, grid, s);
+    case 16: return launch_scan_wc<16, CFG>(a, pred64, grid, s);
+    case 32: return launch_scan_wc<32, CFG>(a, pred64, grid, s);
+    case 48: return launch_scan_wc<48, CFG>(a, pred64, grid, s);
+    case 64: return launch_scan_wc<64, CFG>(a, pred64, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t s) {
+    switch (variant) {
+    case 0: return launch_scan_c<ScanV0>(a, window, pred64, grid, s);
+#ifdef SDFS_SCAN_SWEEP
+#define SWEEP_CASE(id, T) \
+    case id: return window == 48 ? launch_scan_wc<48, T>(a, pred64, grid, s) : hipErrorInvalidValue;
+    SWEEP_CASE(1, ScanV1) SWEEP_CASE(2, ScanV2) SWEEP_CASE(3, ScanV3) SWEEP_CASE(4, ScanV4)
+    SWEEP_CASE(5, ScanV5) SWEEP_CASE(6, ScanV6) SWEEP_CASE(7, ScanV7) SWEEP_CASE(8, ScanV8)
+    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16) SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3)
+    SWEEP_CASE(14, ScanA4) SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15)
+#undef SWEEP_CASE
+#endif
     default: return hipErrorInvalidValue;
     }
 }
