@@ -129,7 +129,8 @@ int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uin
  * d_data: device bytes, 64-byte aligned.  Uniform layout: nbuf buffers of uniform_len bytes
  * (a multiple of 64) at b*uniform_len — the SDFS write-buffer case (every flushed buffer is
  * CHUNK_LENGTH bytes, WritableCacheBuffer.java:115).  buffer_id_base is added to b in the
- * record table.  stream: hipStream_t or NULL (= the engine's own stream).  Asynchronous:
+ * record table.  stream: the hipStream_t to enqueue on (NULL = the HIP null stream, as in every
+ * HIP API).  Asynchronous:
  * returns after enqueueing; d_offs/d_lens are ignored (pass NULL). */
 int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs,
                         const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len,
@@ -151,7 +152,8 @@ int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns);
 int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int n);
 
 /* Synthetic input generator, device side: fills d_out[0..n) with byte
- * (offset+i) of stream `stream` (counter-based SplitMix64; same bytes as the CPU definition). */
+ * (offset+i) of stream `stream` (counter-based SplitMix64; same bytes as the CPU definition),
+ * enqueued on stream_handle (NULL = the HIP null stream). */
 int sdfs_cdc_synth_device(sdfs_cdc_engine* e, uint8_t* d_out, uint64_t n, uint64_t seed,
                           uint64_t stream, uint64_t offset, void* stream_handle);
 

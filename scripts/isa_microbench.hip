@@ -39,12 +39,41 @@ __global__ __launch_bounds__(256) void kvalu(uint32_t* out, int iters, uint32_t 
     if constexpr (OP == 9) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a##k) : "v"(b), "s"(0x06050400u));          \
     if constexpr (OP == 10) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a##k) : "v"(a0), "v"(a1)); \
     if constexpr (OP == 11) asm volatile("v_and_b32 %0, 0xfff, %0" : "+v"(a##k));                            \
-    if constexpr (OP == 12) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a##k));
+    if constexpr (OP == 12) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a##k));                           \
+    if constexpr (OP == 13) asm volatile("v_alignbyte_b32 %0, %0, %1, 1" : "+v"(a##k) : "v"(b));              \
+    if constexpr (OP == 14) asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(a##k) : "v"(b));              \
+    if constexpr (OP == 15) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##k) : "v"(b));             \
+    if constexpr (OP == 16) asm volatile("v_mov_b32 %0, %1" : "=v"(a##k) : "v"(b));                           \
+    if constexpr (OP == 17) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a##k) : "v"(b));                  \
+    if constexpr (OP == 18) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(a##k) : "v"(b), "v"(c));          \
+    if constexpr (OP == 19) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a##k) : "v"(b), "v"(c));
+
             R8(OPX)
 #undef OPX
         }
     }
     out[blockIdx.x * 256 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
+// 64-bit shifts on register pairs: v_lshrrev_b64 / v_lshlrev_b64 / v_lshl_add_u64 / v_mov_b64
+template <int OP>
+__global__ __launch_bounds__(256) void kvalu64(uint32_t* out, int iters, uint32_t seed) {
+    uint64_t a0 = threadIdx.x ^ seed, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 * 11, a5 = a0 * 13,
+             a6 = a0 * 17, a7 = a0 * 19;
+    uint64_t b = seed * 0x9E3779B97F4A7C15ull + threadIdx.x;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+#define OPX(k)                                                                                     \
+    if constexpr (OP == 0) asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(a##k));                  \
+    if constexpr (OP == 1) asm volatile("v_lshlrev_b64 %0, 7, %0" : "+v"(a##k));                  \
+    if constexpr (OP == 2) asm volatile("v_lshl_add_u64 %0, %0, 1, %1" : "+v"(a##k) : "v"(b));    \
+    if constexpr (OP == 3) asm volatile("v_mov_b64 %0, %1" : "=v"(a##k) : "v"(b));
+            R8(OPX)
+#undef OPX
+        }
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7);
 }
 
 // candidate chain: v_and + v_cmp(vcc) + v_addc(vcc) per step, 4 independent chains
@@ -118,10 +147,11 @@ int main() {
     const double wave_instr_valu = (double)blocks * 4 * iters * 16 * 8;  // per kernel
     const char* names[] = {"v_add_u32", "v_perm_b32(vvv)", "v_alignbit_b32(vv,imm)", "v_bitop3_b32(vvv)",
                            "v_bfe_u32(v,imm,imm)", "v_lshl_or_b32(v,imm,v)", "v_add3_u32(vvv)", "v_xor_b32",
-                           "v_alignbit_b32 rot(x,x)", "v_perm_b32(vv,lit)", "v_bitop3(a,a0,a1)", "v_and_b32 lit",
-                           "v_lshrrev_b32"};
-    float base_ms = 0;
-    float ms[13];
+                           "v_alignbit_b32 rot(x,x)", "v_perm_b32(vv,sgpr)", "v_bitop3(a,a0,a1)", "v_and_b32 lit",
+                           "v_lshrrev_b32", "v_alignbyte_b32", "v_lshl_add_u32", "v_cndmask_b32 vcc", "v_mov_b32",
+                           "v_mul_u32_u24", "v_or3_b32", "v_and_or_b32"};
+    constexpr int NOPS = 20;
+    float ms[NOPS];
     ms[0] = time_kernel(kvalu<0>, blocks, iters, out);
     ms[1] = time_kernel(kvalu<1>, blocks, iters, out);
     ms[2] = time_kernel(kvalu<2>, blocks, iters, out);
@@ -135,12 +165,23 @@ int main() {
     ms[10] = time_kernel(kvalu<10>, blocks, iters, out);
     ms[11] = time_kernel(kvalu<11>, blocks, iters, out);
     ms[12] = time_kernel(kvalu<12>, blocks, iters, out);
-    base_ms = ms[0];
-    const double ghz = wave_instr_valu * 2.0 / simds / (base_ms * 1e-3) / 1e9;  // assuming add = 2 cyc
-    printf("effective clock if v_add_u32 = 2 cyc/wave-instr: %.2f GHz\n", ghz);
-    for (int i = 0; i < 13; i++)
-        printf("%-28s %8.3f ms  %5.2f cyc/wave-instr/SIMD (rel. to add=2)\n", names[i], ms[i],
-               2.0 * ms[i] / base_ms);
+    ms[13] = time_kernel(kvalu<13>, blocks, iters, out);
+    ms[14] = time_kernel(kvalu<14>, blocks, iters, out);
+    ms[15] = time_kernel(kvalu<15>, blocks, iters, out);
+    ms[16] = time_kernel(kvalu<16>, blocks, iters, out);
+    ms[17] = time_kernel(kvalu<17>, blocks, iters, out);
+    ms[18] = time_kernel(kvalu<18>, blocks, iters, out);
+    ms[19] = time_kernel(kvalu<19>, blocks, iters, out);
+    const float xor_ms = ms[7];  // calibration: a plain 2-operand VALU op = 2 cycles per wave64 on SIMD-32
+    const double ghz = wave_instr_valu * 2.0 / simds / (xor_ms * 1e-3) / 1e9;
+    printf("effective clock if v_xor_b32 = 2 cyc/wave-instr: %.2f GHz\n", ghz);
+    for (int i = 0; i < NOPS; i++)
+        printf("%-28s %8.3f ms  %5.2f cyc/wave-instr/SIMD\n", names[i], ms[i], 2.0 * ms[i] / xor_ms);
+    const char* n64[] = {"v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64", "v_mov_b64"};
+    float m64[4] = {time_kernel(kvalu64<0>, blocks, iters, out), time_kernel(kvalu64<1>, blocks, iters, out),
+                    time_kernel(kvalu64<2>, blocks, iters, out), time_kernel(kvalu64<3>, blocks, iters, out)};
+    for (int i = 0; i < 4; i++)
+        printf("%-28s %8.3f ms  %5.2f cyc/wave-instr/SIMD\n", n64[i], m64[i], 2.0 * m64[i] / xor_ms);
     float mc = time_kernel(kcand, blocks, iters, out);
     const double wi_c = (double)blocks * 4 * iters * 32 * 4 * 3;
     printf("%-28s %8.3f ms  %5.2f cyc/wave-instr (3 instr/step)\n", "and+cmp(vcc)+addc chain", mc,

@@ -19,13 +19,15 @@ from sdfs_amd import HipVariableSha256HashEngine  # noqa: E402
 from sdfs_amd.device import DeviceBatch  # noqa: E402
 
 variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4,5").split(",")]
-segs = [int(v) for v in os.environ.get("SEGS", "2048").split(",")]
+segs = [int(v) for v in os.environ.get("SEGS", "4096").split(",")]
+hvars = [int(v) for v in os.environ.get("HASH_VARIANTS", "0").split(",")]
 steps = int(os.environ.get("STEPS", "5"))
 nbuf = int(os.environ.get("NBUF", "16384"))
 ref = None
 data = None
-for v in variants:
-    for sl in segs:
+for v, sl, hv in [(v, sl, hv) for v in variants for sl in segs for hv in hvars]:
+    if True:
+        os.environ["SDFS_HASH_VARIANT"] = str(hv)
         os.environ["SDFS_SCAN_VARIANT"] = str(v)
         os.environ["SDFS_SEG_LEN"] = str(sl)
         eng = HipVariableSha256HashEngine()
@@ -50,7 +52,7 @@ for v in variants:
             same = bool((counts == ref[0]).all() and (st == ref[1]).all() and (ln == ref[2]).all()
                         and (dg == ref[3]).all())
         nbytes = nbuf * 262144
-        print(json.dumps(dict(variant=v, seg_len=sl, scan_ms=round(kt["cdc_scan"], 4),
+        print(json.dumps(dict(variant=v, hash_variant=hv, seg_len=sl, scan_ms=round(kt["cdc_scan"], 4),
                               scan_gbps=round(nbytes / kt["cdc_scan"] / 1e6, 1),
                               hash_ms=round(kt["chunk_hash"], 4), resolve_ms=round(kt["cdc_resolve"], 4),
                               identical_to_v0=same, chunks=total)), flush=True)

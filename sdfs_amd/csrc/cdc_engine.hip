@@ -105,6 +105,7 @@ struct sdfs_cdc_engine {
     int num_cus = 256;
     uint32_t seg_len = 4096;  // bytes of one buffer per lane (multiple of the variant's block)
     int scan_variant = 0;
+    int hash_variant = 0;
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
@@ -143,7 +144,8 @@ namespace {
 int validate(const sdfs_cdc_params* p) {
     if (!p) return fail(SDFS_CDC_EINVAL, "null params");
     const int d = poly_degree(p->poly);
-    if (d < 40 || d > 55) return fail(SDFS_CDC_EINVAL, "polynomial degree %d outside [40,55]", d);
+    // fp < 2^d lives in two dwords with the push index (bits d-8..d-1) inside the high one
+    if (d < 48 || d > 55) return fail(SDFS_CDC_EINVAL, "polynomial degree %d outside [48,55]", d);
     if (!scan_window_supported((int)p->window))
         return fail(SDFS_CDC_EINVAL, "window %u unsupported (16/32/48/64)", p->window);
     if (p->max_len == 0) return fail(SDFS_CDC_EINVAL, "max_len must be > 0");
@@ -297,7 +299,7 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
     ha.buffer_id_base = buffer_id_base;
     ha.algo = e->prm.hash_algo;
     // upper bound on chunks: every buffer at most cap
-    HIP_TRY(launch_hash(ha, nslots, s));
+    HIP_TRY(launch_hash(ha, nslots, e->hash_variant, s));
     if (timing) {
         HIP_TRY(hipEventRecord(e->ev[6], s));
         e->runs_recorded++;
@@ -446,6 +448,7 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     // tuning overrides for experiments (DESIGN.md "Scan variants"); production uses variant 0
     if (const char* v = getenv("SDFS_SCAN_VARIANT")) e->scan_variant = atoi(v);
     if (const char* v = getenv("SDFS_SEG_LEN")) e->seg_len = (uint32_t)atoi(v);
+    if (const char* v = getenv("SDFS_HASH_VARIANT")) e->hash_variant = atoi(v);
     e->scan_info = scan_variant_info(e->scan_variant);
     if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0) {
         sdfs_cdc_destroy(e);
@@ -507,7 +510,7 @@ int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_
         return fail(SDFS_CDC_EINVAL, "sdfs_cdc_run_device: ragged layouts need sdfs_cdc_run_device_ragged");
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
-    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e->stream;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     return run_pipeline(e, d_data, 0, d_offs, d_lens, nbuf, uniform_len, buffer_id_base, out, s);
 }
 
@@ -517,7 +520,7 @@ int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64
     if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
-    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e->stream;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     return run_pipeline(e, d_data, data_bytes, d_offs, d_lens, nbuf, 0, buffer_id_base, out, s);
 }
 
@@ -610,7 +613,7 @@ int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uin
     ha.cap = 1;
     ha.digests = e->o_digests.p;
     ha.algo = e->prm.hash_algo;
-    HIP_TRY(launch_hash(ha, 1, s));
+    HIP_TRY(launch_hash(ha, 1, 0, s));
     HIP_TRY(hipMemcpyAsync(ctl + 4, e->o_digests.p, 32, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     memcpy(digest, ctl + 4, e->digest_len);
@@ -621,7 +624,7 @@ int sdfs_cdc_synth_device(sdfs_cdc_engine* e, uint8_t* d_out, uint64_t n, uint64
                           uint64_t offset, void* stream_handle) {
     if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
     HIP_TRY(hipSetDevice(e->prm.device));
-    hipStream_t s = stream_handle ? reinterpret_cast<hipStream_t>(stream_handle) : e->stream;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_handle);  // NULL = the HIP null stream
     HIP_TRY(launch_synth(d_out, n, seed, stream, offset, s));
     return SDFS_CDC_OK;
 }

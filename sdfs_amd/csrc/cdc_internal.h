@@ -113,7 +113,7 @@ hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, 
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);
-hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, hipStream_t stream);
+hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
                         hipStream_t stream);
 bool scan_window_supported(int window);

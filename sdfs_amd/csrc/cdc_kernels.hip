@@ -22,6 +22,11 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
+// (a & b) | c.  v_bitop3 truth-table bit index is (A << 2) | (B << 1) | C (the encoding hipcc
+// itself emits for Ch, bitop3:0xE4 = C ? A : B).
+__device__ __forceinline__ uint32_t bitop3_and_or(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xEA);
+}
 
 // ------------------------------------------------------------------------------------------
 // 1. candidate scan
@@ -37,8 +42,10 @@ __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
 template <int P, int Q, int ABL = 0>
 __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
                                           uint32_t push_base, uint32_t jshift, const uint8_t* tab) {
-    const uint32_t j = __builtin_amdgcn_ubfe(hi, jshift, 8);
-    const uint32_t pa = (j << 8) | push_base;                                          // push[j], lane copy
+    // push[j] address (j << 8) | push_base with j = (fp >> (d-8)) & 0xFF = hi bits [jshift, jshift+8):
+    // one full-rate shift + one v_bitop3 ((A & B) | C, table 0xEA) instead of v_bfe + v_lshl_or
+    // (both half-rate on gfx950, scripts/isa_microbench.hip).
+    const uint32_t pa = bitop3_and_or(hi >> (jshift - 8), 0xFF00u, push_base);
     const uint32_t qa = __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + Q) << 8));  // (o << 8) | c8
     const uint2 pv = (ABL & 2) ? make_uint2(pa, pa >> 3) : *reinterpret_cast<const uint2*>(tab + pa);
     const uint2 qv = (ABL & 1) ? make_uint2(qa, qa >> 3) : *reinterpret_cast<const uint2*>(tab + qa);
@@ -52,8 +59,7 @@ __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t d
 template <int P>
 __device__ __forceinline__ void push_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t push_base,
                                           uint32_t jshift, const uint8_t* tab) {
-    const uint32_t j = __builtin_amdgcn_ubfe(hi, jshift, 8);
-    const uint2 pv = *reinterpret_cast<const uint2*>(tab + ((j << 8) | push_base));
+    const uint2 pv = *reinterpret_cast<const uint2*>(tab + bitop3_and_or(hi >> (jshift - 8), 0xFF00u, push_base));
     const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);
     const uint32_t nlo = __builtin_amdgcn_perm(lo, dw, 0x06050400u | P);
     lo = nlo ^ pv.x;
@@ -709,7 +715,9 @@ __device__ __forceinline__ void tail_words(uint32_t (&m)[16], const uint8_t* t, 
     }
 }
 
-template <int ALGO>
+// ABL (sweep builds only): 1 = synthesize the message words instead of loading them, 2 = skip the
+// compression (fold the loaded words instead).  Production ABL = 0.
+template <int ALGO, int ABL = 0>
 __global__ __launch_bounds__(256) void chunk_hash_kernel(HashArgs a) {
     constexpr bool SHA = ALGO != 2;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -740,7 +748,10 @@ __global__ __launch_bounds__(256) void chunk_hash_kernel(HashArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 uint4 v;
-                __builtin_memcpy(&v, p + 64 * blk + 16 * q, 16);  // unaligned global_load_dwordx4
+                if constexpr (ABL & 1)
+                    v = make_uint4(s[q] + blk, s[q + 4] ^ blk, s[q] * 3u, s[q + 4] + q);
+                else
+                    __builtin_memcpy(&v, p + 64 * blk + 16 * q, 16);  // unaligned global_load_dwordx4
                 w[4 * q] = SHA ? __builtin_bswap32(v.x) : v.x;
                 w[4 * q + 1] = SHA ? __builtin_bswap32(v.y) : v.y;
                 w[4 * q + 2] = SHA ? __builtin_bswap32(v.z) : v.z;
@@ -758,7 +769,10 @@ __global__ __launch_bounds__(256) void chunk_hash_kernel(HashArgs a) {
                 w[15] = SHA ? (uint32_t)bits : (uint32_t)(bits >> 32);
             }
         }
-        if constexpr (SHA) {
+        if constexpr (ABL & 2) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) s[j & 7] ^= w[j];
+        } else if constexpr (SHA) {
             sha256_compress(s, w);
         } else {
             uint32_t m4[4] = {s[0], s[1], s[2], s[3]};
@@ -792,9 +806,20 @@ __global__ __launch_bounds__(256) void chunk_hash_kernel(HashArgs a) {
     }
 }
 
-hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, hipStream_t s) {
+hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t s) {
     const uint32_t blocks = (uint32_t)((max_tasks + 255) / 256);
     if (blocks == 0) return hipSuccess;
+#ifdef SDFS_SCAN_SWEEP
+    if (variant == 1 && a.algo == 0) {
+        hipLaunchKernelGGL((chunk_hash_kernel<0, 1>), dim3(blocks), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    if (variant == 2 && a.algo == 0) {
+        hipLaunchKernelGGL((chunk_hash_kernel<0, 2>), dim3(blocks), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+#endif
+    if (variant != 0) return hipErrorInvalidValue;
     switch (a.algo) {
     case 0: hipLaunchKernelGGL((chunk_hash_kernel<0>), dim3(blocks), dim3(256), 0, s, a); break;
     case 1: hipLaunchKernelGGL((chunk_hash_kernel<1>), dim3(blocks), dim3(256), 0, s, a); break;

@@ -235,15 +235,15 @@ class HipVariableSha256HashEngine:
     def run_device(self, data_ptr: int, nbuf: int, uniform_len: int, out: _lib.DevOut, stream: int = 0,
                    buffer_id_base: int = 0) -> None:
         check(self._lib.sdfs_cdc_run_device(self._h, data_ptr, None, None, nbuf, uniform_len, buffer_id_base,
-                                            ctypes.byref(out), stream or None))
+                                            ctypes.byref(out), stream))
 
     def run_device_ragged(self, data_ptr: int, data_bytes: int, offs_ptr: int, lens_ptr: int, nbuf: int,
                           out: _lib.DevOut, stream: int = 0, buffer_id_base: int = 0) -> None:
         check(self._lib.sdfs_cdc_run_device_ragged(self._h, data_ptr, data_bytes, offs_ptr, lens_ptr, nbuf,
-                                                   buffer_id_base, ctypes.byref(out), stream or None))
+                                                   buffer_id_base, ctypes.byref(out), stream))
 
     def synth_device(self, ptr: int, n: int, seed: int, stream_id: int, offset: int = 0, stream: int = 0):
-        check(self._lib.sdfs_cdc_synth_device(self._h, ptr, n, seed, stream_id, offset, stream or None))
+        check(self._lib.sdfs_cdc_synth_device(self._h, ptr, n, seed, stream_id, offset, stream))
 
     def sync(self) -> None:
         check(self._lib.sdfs_cdc_stream_sync(self._h))
