@@ -119,6 +119,42 @@ __global__ __launch_bounds__(256) void klds(uint32_t* out, int iters, uint32_t s
     out[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+// dependent-chain latency: ONE accumulator per lane, one wave per SIMD
+template <int OP>
+__global__ __launch_bounds__(256) void klat(uint32_t* out, int iters, uint32_t seed) {
+    uint32_t a = threadIdx.x ^ seed;
+    const uint32_t b = seed * 0x9E3779B9u + threadIdx.x, c = b ^ 0x5A5A5A5Au;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int u = 0; u < 64; u++) {
+            if constexpr (OP == 0) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(b));
+            if constexpr (OP == 1) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a) : "v"(b));
+            if constexpr (OP == 2) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a) : "v"(b), "v"(c));
+            if constexpr (OP == 3) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+            if constexpr (OP == 4) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a));
+            if constexpr (OP == 5) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+            if constexpr (OP == 6) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+        }
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = a;
+}
+
+// dependent LDS round trip: address from the previous load's value
+__global__ __launch_bounds__(256) void klatlds(uint32_t* out, int iters, uint32_t seed) {
+    __shared__ uint2 tab[8192];
+    for (int i = threadIdx.x; i < 8192; i += 256) tab[i] = make_uint2((i * 8 + 8) & 0xFFF8, i);
+    __syncthreads();
+    uint32_t a = (threadIdx.x & 31) << 3;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(tab) + a);
+            a = v.x;
+        }
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = a;
+}
+
 template <typename K>
 float time_kernel(K kern, int blocks, int iters, uint32_t* out) {
     hipEvent_t a, b;
@@ -182,6 +218,20 @@ int main() {
                     time_kernel(kvalu64<2>, blocks, iters, out), time_kernel(kvalu64<3>, blocks, iters, out)};
     for (int i = 0; i < 4; i++)
         printf("%-28s %8.3f ms  %5.2f cyc/wave-instr/SIMD\n", n64[i], m64[i], 2.0 * m64[i] / xor_ms);
+    {
+        const char* ln[] = {"v_xor_b32", "v_alignbit_b32", "v_bitop3_b32", "v_perm_b32", "v_lshrrev_b32",
+                            "v_add3_u32", "v_add_u32"};
+        const int lb = cus;  // one 256-thread block per CU = one wave per SIMD
+        const int li = 200;
+        float lm[7] = {time_kernel(klat<0>, lb, li, out), time_kernel(klat<1>, lb, li, out),
+                       time_kernel(klat<2>, lb, li, out), time_kernel(klat<3>, lb, li, out),
+                       time_kernel(klat<4>, lb, li, out), time_kernel(klat<5>, lb, li, out),
+                       time_kernel(klat<6>, lb, li, out)};
+        for (int i = 0; i < 7; i++)
+            printf("dependent %-18s %6.1f cycles/instr (1 wave/SIMD)\n", ln[i], lm[i] * 1e-3 * ghz * 1e9 / (li * 64.0));
+        float ll = time_kernel(klatlds, lb, li, out);
+        printf("dependent ds_read_b64 round trip %6.1f cycles\n", ll * 1e-3 * ghz * 1e9 / (li * 16.0));
+    }
     float mc = time_kernel(kcand, blocks, iters, out);
     const double wi_c = (double)blocks * 4 * iters * 32 * 4 * 3;
     printf("%-28s %8.3f ms  %5.2f cyc/wave-instr (3 instr/step)\n", "and+cmp(vcc)+addc chain", mc,

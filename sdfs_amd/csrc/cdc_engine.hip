@@ -114,6 +114,7 @@ struct sdfs_cdc_engine {
     std::mutex mu;  // one engine context: calls are serialised (DESIGN.md "Host edge")
 
     DevBuf<uint8_t> tab_image;
+    DevBuf<uint8_t> zero_page;
     // workspace for run_device
     DevBuf<uint32_t> bitmap;
     DevBuf<uint64_t> seg_prefix;
@@ -221,6 +222,7 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
     sa.val_lo = (uint32_t)e->prm.pred_value;
     sa.val_hi = (uint32_t)(e->prm.pred_value >> 32);
     sa.tab_image = e->tab_image.p;
+    sa.zero_page = e->zero_page.p;
     uint64_t seg_bound;
     if (uniform_len) {
         const uint64_t spb = (uniform_len + e->seg_len - 1) / e->seg_len;
@@ -455,7 +457,8 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
         return fail(SDFS_CDC_EINVAL, "bad scan variant/segment length");
     }
     std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies);
-    if (e->tab_image.ensure(img.size()) != hipSuccess ||
+    if (e->zero_page.ensure(256) != hipSuccess || hipMemset(e->zero_page.p, 0, 256) != hipSuccess ||
+        e->tab_image.ensure(img.size()) != hipSuccess ||
         hipMemcpy(e->tab_image.p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
         sdfs_cdc_destroy(e);
         return fail(SDFS_CDC_ENOMEM, "table upload failed");
@@ -471,6 +474,7 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
         (void)hipSetDevice(e->prm.device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
         e->tab_image.release();
+        e->zero_page.release();
         e->bitmap.release();
         e->seg_prefix.release();
         e->small.release();

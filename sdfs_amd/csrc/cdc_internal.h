@@ -41,6 +41,7 @@ struct ScanArgs {
     uint32_t jshift;             // deg(P) - 40 : bit offset of the push index inside the hi word
     uint32_t mask_lo, mask_hi, val_lo, val_hi;
     const uint8_t* tab_image;    // global copy of the LDS image (scan_lds_bytes(copies))
+    const uint8_t* zero_page;    // 256 zero bytes (branch-free prefetch of tail blocks)
 };
 
 struct ResolveArgs {

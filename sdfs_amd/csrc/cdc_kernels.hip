@@ -177,6 +177,36 @@ __device__ __forceinline__ void block_words(uint32_t (&words)[NCH][NW], uint32_t
     }
 }
 
+// Branch-free block load for software prefetch: a block that is not wholly readable (buffer tail,
+// or no block at all) is fetched from the 128-byte device zero page instead, so no control flow
+// separates the load from its use one iteration later (hipcc puts an s_waitcnt vmcnt(0) at
+// every control-flow merge after a load).  `full` records whether the fast load was valid;
+// tail blocks are re-read by fix_block when they become current.
+template <int N>
+__device__ __forceinline__ bool load_block_nb(uint32_t (&d)[N], const uint8_t* data, const uint8_t* zero_page,
+                                              uint64_t addr, uint64_t lim) {
+    const bool full = addr + 4 * N <= lim;
+    const uint4* p = reinterpret_cast<const uint4*>(full ? data + addr : zero_page);
+#pragma unroll
+    for (int i = 0; i < N / 4; i++) {
+        const uint4 v = p[i];
+        d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+    }
+    return full;
+}
+
+template <int N>
+__device__ __forceinline__ void fix_block(uint32_t (&d)[N], bool full, const uint8_t* data, uint64_t addr,
+                                          uint64_t lim) {
+    if (!__all(full)) {  // rare: some lane's block is a buffer tail
+        if (!full) {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(data + addr);
+#pragma unroll
+            for (int i = 0; i < N; i++) d[i] = (addr + 4 * i < lim) ? p[i] : 0u;
+        }
+    }
+}
+
 // Scan variants (DESIGN.md "Rabin scan"): C lane-private table copies (32: conflict-free,
 // 128 KiB, one 1024-thread workgroup per CU; 16: 2-way, 64 KiB, two workgroups per CU), NCH
 // independent segments per lane, BLK bytes per lane per iteration (128 = one whole cache line
@@ -254,6 +284,7 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
 
         uint32_t lo[NCH], hi[NCH];
         uint32_t prev[NCH][16], cur[NCH][BLKW];
+        bool cur_full[NCH];
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             if (nblk[c] != 0 && !first[c]) {
@@ -266,17 +297,20 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
             warm_from<W, 64 - W>(lo[c], hi[c], prev[c], push_base, a.jshift, tab);
             if constexpr (CFG::kPrefetch) {
                 const bool act = nblk[c] != 0;
-                load_block<BLKW>(cur[c], a.data, act ? start[c] : 0, act ? end[c] : 0);
+                cur_full[c] = load_block_nb<BLKW>(cur[c], a.data, a.zero_page, act ? start[c] : 0, act ? end[c] : 0);
             }
         }
 
         for (uint32_t blk = 0; blk < maxblk; blk++) {
             uint32_t nxt[NCH][CFG::kPrefetch ? BLKW : 1];
+            bool nxt_full[NCH];
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 if constexpr (CFG::kPrefetch) {
+                    fix_block<BLKW>(cur[c], cur_full[c], a.data, start[c] + (uint64_t)BLK * blk, end[c]);
                     const bool act = blk + 1 < nblk[c];
-                    load_block<BLKW>(nxt[c], a.data, act ? start[c] + (uint64_t)BLK * (blk + 1) : 0, act ? end[c] : 0);
+                    nxt_full[c] = load_block_nb<BLKW>(nxt[c], a.data, a.zero_page,
+                                                      act ? start[c] + (uint64_t)BLK * (blk + 1) : 0, act ? end[c] : 0);
                 } else if constexpr (CFG::kAbl & 8) {
 #pragma unroll
                     for (int i = 0; i < BLKW; i++) cur[c][i] = prev[c][i & 15] * 0x9E3779B1u + blk;
@@ -313,6 +347,7 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
                 if constexpr (CFG::kPrefetch) {
 #pragma unroll
                     for (int i = 0; i < BLKW; i++) cur[c][i] = nxt[c][i];
+                    cur_full[c] = nxt_full[c];
                 }
             }
         }
@@ -324,6 +359,7 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
 // (measured 1.56 ms / 4 GiB on MI355X vs 2.6 ms with 64-byte loads, DESIGN.md "Scan variants").
 using ScanV0 = ScanCfg<32, 1, false, 4, 0, 128>;
 using ScanV16 = ScanCfg<32, 2, false, 4>;  // round-1 first version: 64-byte loads, 2 chains
+using ScanV17 = ScanCfg<32, 2, true, 4, 0, 128>;
 using ScanV1 = ScanCfg<32, 2, true, 4>;
 using ScanV2 = ScanCfg<32, 1, true, 4>;
 using ScanV3 = ScanCfg<16, 1, true, 8>;
@@ -335,12 +371,13 @@ using ScanV8 = ScanCfg<16, 1, false, 8, 0, 128>;
 using ScanV9 = ScanCfg<32, 1, true, 4, 0, 128>;
 using ScanV10 = ScanCfg<32, 1, false, 4, 0, 256>;
 using ScanV15 = ScanCfg<32, 2, false, 4, 0, 256>;
-using ScanA1 = ScanCfg<32, 2, false, 4, 1>;   // no pop read
-using ScanA2 = ScanCfg<32, 2, false, 4, 2>;   // no push read
-using ScanA3 = ScanCfg<32, 2, false, 4, 3>;   // no LDS at all
-using ScanA4 = ScanCfg<32, 2, false, 4, 4>;   // no candidate test
-using ScanA8 = ScanCfg<32, 2, false, 4, 8>;   // no global loads
-using ScanA15 = ScanCfg<32, 2, false, 4, 15>; // only the rolling arithmetic
+// ablations of the production configuration (ids 11..25)
+using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;   // no pop read
+using ScanA2 = ScanCfg<32, 1, false, 4, 2, 128>;   // no push read
+using ScanA3 = ScanCfg<32, 1, false, 4, 3, 128>;   // no LDS at all
+using ScanA4 = ScanCfg<32, 1, false, 4, 4, 128>;   // no candidate test
+using ScanA8 = ScanCfg<32, 1, false, 4, 8, 128>;   // no global loads
+using ScanA15 = ScanCfg<32, 1, false, 4, 15, 128>; // only the rolling arithmetic
 
 template <class CFG>
 constexpr ScanVariantInfo info_of() {
@@ -363,6 +400,7 @@ ScanVariantInfo scan_variant_info(int v) {
     case 10: return info_of<ScanV10>();
     case 15: return info_of<ScanV15>();
     case 16: return info_of<ScanV16>();
+    case 17: return info_of<ScanV17>();
     case 11: return info_of<ScanA1>();
     case 12: return info_of<ScanA2>();
     case 13: return info_of<ScanA3>();
@@ -406,7 +444,7 @@ hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, 
     case id: return window == 48 ? launch_scan_wc<48, T>(a, pred64, grid, s) : hipErrorInvalidValue;
     SWEEP_CASE(1, ScanV1) SWEEP_CASE(2, ScanV2) SWEEP_CASE(3, ScanV3) SWEEP_CASE(4, ScanV4)
     SWEEP_CASE(5, ScanV5) SWEEP_CASE(6, ScanV6) SWEEP_CASE(7, ScanV7) SWEEP_CASE(8, ScanV8)
-    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16) SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3)
+    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16) SWEEP_CASE(17, ScanV17) SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3)
     SWEEP_CASE(14, ScanA4) SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15)
 #undef SWEEP_CASE
 #endif
