@@ -141,6 +141,12 @@ int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_
 int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
                                const uint64_t* d_offs, const uint32_t* d_lens, uint32_t nbuf,
                                uint64_t buffer_id_base, const sdfs_cdc_dev_out* out, void* stream);
+/* Sub-batch pipelining of sdfs_cdc_run_device (uniform layouts): split a batch into up to
+ * `parts` (1..16) sub-batches of at least part_min_bytes, so the candidate scan of one overlaps
+ * the fingerprinting of the previous on the same CUs (engine-internal streams, joined back to the
+ * caller's stream).  parts = 1 runs everything on the caller's stream.  Default 1 (measured
+ * slower on MI355X when split) / 512 MiB. */
+int sdfs_cdc_set_pipeline(sdfs_cdc_engine* e, int parts, uint64_t part_min_bytes);
 /* Block until the engine's own stream has drained. */
 int sdfs_cdc_stream_sync(sdfs_cdc_engine* e);
 

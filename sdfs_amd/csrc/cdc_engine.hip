@@ -93,9 +93,14 @@ struct DevBuf {
     }
 };
 
-constexpr int kNumTimed = 6;
+// timed stages (kernel_times order); "pipeline" = device time from the first enqueue to the last
+// kernel of the run on the caller's stream (the stages overlap when the run is sub-batched)
+constexpr int kNumTimed = 7;
 const char* kKernelNames[kNumTimed] = {"prep", "cdc_scan", "cdc_resolve", "cdc_prefix", "cdc_scatter",
-                                       "chunk_hash"};
+                                       "chunk_hash", "pipeline"};
+enum { K_PREP = 0, K_SCAN, K_RESOLVE, K_PREFIX, K_SCATTER, K_HASH, K_PIPE };
+constexpr int kMaxParts = 16;
+constexpr int kEvPerRun = 2 * (kMaxParts * 5 + 2);
 
 }  // namespace
 
@@ -134,10 +139,24 @@ struct sdfs_cdc_engine {
     size_t pin_out_n = 0;
 
     // per-kernel HIP events for the last `timing_slots` runs (ring); averaged by kernel_times
+    struct TimedRun {
+        std::vector<hipEvent_t> ev;  // kEvPerRun events
+        std::vector<int> kid;        // stage id of event pair i (ev[2i], ev[2i+1])
+    };
     int timing_slots = 0;
-    std::vector<std::vector<hipEvent_t>> ev_runs;
+    std::vector<TimedRun> ev_runs;
     uint64_t runs_recorded = 0;
-    hipEvent_t* ev = nullptr;  // event set of the run in flight (nullptr: timing off)
+    TimedRun* run = nullptr;  // run in flight (nullptr: timing off)
+
+    // sub-batch pipeline: scan of part k+1 on s_scan overlaps resolve..hash of part k on s_post.
+    // Measured NEGATIVE on MI355X (4 GiB step: 1 part 4.84 ms, 2 parts 7.0, 4 parts 9.7, 8 parts
+    // 17.4: the persistent 128 KiB-LDS scan workgroups and the hash workgroups starve each other
+    // in the dispatcher), so the default is 1 part; kept for experiments.
+    int parts = 1;
+    uint64_t part_min_bytes = 512ull << 20;
+    hipStream_t s_scan = nullptr, s_post = nullptr;
+    hipEvent_t ev_in = nullptr, ev_done = nullptr;
+    hipEvent_t ev_scan[kMaxParts] = {};
 };
 
 namespace {
@@ -173,7 +192,23 @@ uint32_t slot_cap_for(const sdfs_cdc_params& p, uint64_t len) {
     return (uint32_t)(len / shortest + 2);
 }
 
-// The device pipeline on `s`.  Caller holds e->mu and has selected the device.
+// Records a start event for stage `kid` on stream `st` (timing runs only); returns the pair index.
+int t_begin(sdfs_cdc_engine* e, int kid, hipStream_t st) {
+    if (!e->run) return -1;
+    const int i = (int)e->run->kid.size();
+    if (2 * i + 1 >= kEvPerRun) return -1;
+    e->run->kid.push_back(kid);
+    (void)hipEventRecord(e->run->ev[2 * i], st);
+    return i;
+}
+void t_end(sdfs_cdc_engine* e, int i, hipStream_t st) {
+    if (e->run && i >= 0) (void)hipEventRecord(e->run->ev[2 * i + 1], st);
+}
+
+// The device pipeline, enqueued behind everything already on `s` and completing on `s`.  Large
+// uniform batches are split into `parts` sub-batches: the scan of part k+1 (engine stream
+// s_scan) overlaps resolve/prefix/scatter/hash of part k (s_post), so the latency-bound scan and
+// the VALU-bound hash share the CUs (DESIGN.md "Pipeline").  Caller holds e->mu.
 int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
                  const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
                  const sdfs_cdc_dev_out* out, hipStream_t s) {
@@ -185,127 +220,187 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
     if (uniform_len) data_bytes = (uint64_t)nbuf * uniform_len;
     if (uniform_len && out->cap < slot_cap_for(e->prm, uniform_len))
         return fail(SDFS_CDC_ECAP, "cap %u < slot_cap %u", out->cap, slot_cap_for(e->prm, uniform_len));
-    e->ev = nullptr;
-    if (e->timing_slots > 0) e->ev = e->ev_runs[e->runs_recorded % e->timing_slots].data();
-    const bool timing = e->ev != nullptr;
-    if (timing) HIP_TRY(hipEventRecord(e->ev[0], s));
+
+    e->run = nullptr;
+    if (e->timing_slots > 0) {
+        e->run = &e->ev_runs[e->runs_recorded % e->timing_slots];
+        e->run->kid.clear();
+    }
+    const int tpipe = t_begin(e, K_PIPE, s);
     if (nbuf == 0) {
         HIP_TRY(hipMemsetAsync(out->total, 0, 4, s));
-        if (timing)
-            for (int i = 1; i <= kNumTimed; i++) HIP_TRY(hipEventRecord(e->ev[i], s));
-        if (timing) e->runs_recorded++;
+        t_end(e, tpipe, s);
+        if (e->run) e->runs_recorded++;
         return SDFS_CDC_OK;
     }
+
+    // sub-batch split (uniform layout only): parts of whole buffers, each >= part_min_bytes
+    uint32_t parts = 1;
+    if (uniform_len && e->parts > 1) {
+        const uint64_t by_size = data_bytes / std::max<uint64_t>(e->part_min_bytes, 1);
+        parts = (uint32_t)std::min<uint64_t>({(uint64_t)e->parts, by_size, (uint64_t)nbuf, (uint64_t)kMaxParts});
+        parts = std::max<uint32_t>(parts, 1);
+    }
+
     // workspace
     const uint64_t nwords = ((data_bytes + 63) / 64) * 2 + 2;
     HIP_TRY(e->bitmap.ensure(nwords));
-    HIP_TRY(e->small.ensure(2 * kMaxBins + 4));
+    constexpr uint32_t kSmall = 2 * kMaxBins + 8;  // hist | cursor | overflow, total, base_in, base_out ..
+    HIP_TRY(e->small.ensure((uint64_t)kSmall * parts + 8));
     HIP_TRY(e->rec_base.ensure(nbuf));
     const uint64_t nslots = (uint64_t)nbuf * out->cap;
     HIP_TRY(e->tasks.ensure(nslots));
-    uint32_t* hist = e->small.p;
-    uint32_t* cursor = e->small.p + kMaxBins;
-    uint32_t* overflow = e->small.p + 2 * kMaxBins;
-    HIP_TRY(hipMemsetAsync(e->small.p, 0, (2 * kMaxBins + 4) * sizeof(uint32_t), s));
-
-    ScanArgs sa{};
-    sa.data = d_data;
-    sa.offs = d_offs;
-    sa.lens = d_lens;
-    sa.bitmap = e->bitmap.p;
-    sa.nbuf = nbuf;
-    sa.uniform_len = uniform_len;
-    sa.seg_len = e->seg_len;
-    sa.jshift = (uint32_t)(e->degree - 40);
-    sa.mask_lo = (uint32_t)e->prm.pred_mask;
-    sa.mask_hi = (uint32_t)(e->prm.pred_mask >> 32);
-    sa.val_lo = (uint32_t)e->prm.pred_value;
-    sa.val_hi = (uint32_t)(e->prm.pred_value >> 32);
-    sa.tab_image = e->tab_image.p;
-    sa.zero_page = e->zero_page.p;
-    uint64_t seg_bound;
-    if (uniform_len) {
-        const uint64_t spb = (uniform_len + e->seg_len - 1) / e->seg_len;
-        sa.total_segs = spb * nbuf;
-        seg_bound = sa.total_segs;
-    } else {
-        HIP_TRY(e->seg_prefix.ensure((uint64_t)nbuf + 1));
-        HIP_TRY(launch_seg_prefix(d_lens, nbuf, e->seg_len, e->seg_prefix.p, s));
-        sa.seg_prefix = e->seg_prefix.p;
-        seg_bound = data_bytes / e->seg_len + nbuf;
+    uint32_t* running = e->small.p + (uint64_t)kSmall * parts;  // running record base per part
+    hipStream_t sscan = parts > 1 ? e->s_scan : s;
+    hipStream_t spost = parts > 1 ? e->s_post : s;
+    if (parts > 1) {
+        HIP_TRY(hipEventRecord(e->ev_in, s));
+        HIP_TRY(hipStreamWaitEvent(sscan, e->ev_in, 0));
+        HIP_TRY(hipStreamWaitEvent(spost, e->ev_in, 0));
     }
-    if (timing) HIP_TRY(hipEventRecord(e->ev[1], s));
-    const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
-    uint64_t grid = (seg_bound + per_block - 1) / per_block;
-    grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus * e->scan_info.wg_per_cu);
-    grid = std::max<uint64_t>(grid, 1);
+    {
+        const int t = t_begin(e, K_PREP, spost);
+        HIP_TRY(hipMemsetAsync(e->small.p, 0, ((uint64_t)kSmall * parts + 8) * sizeof(uint32_t), spost));
+        if (!uniform_len) {
+            HIP_TRY(e->seg_prefix.ensure((uint64_t)nbuf + 1));
+            HIP_TRY(launch_seg_prefix(d_lens, nbuf, e->seg_len, e->seg_prefix.p, spost));
+        }
+        t_end(e, t, spost);
+    }
+    if (!uniform_len && sscan != spost) return fail(SDFS_CDC_EINVAL, "internal: ragged batches are not split");
+
     const bool pred64 = (e->prm.pred_mask >> 32) != 0;
-    HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, s));
-    if (timing) HIP_TRY(hipEventRecord(e->ev[2], s));
+    for (uint32_t p = 0; p < parts; p++) {
+        const uint32_t b0 = (uint32_t)((uint64_t)nbuf * p / parts);
+        const uint32_t b1 = (uint32_t)((uint64_t)nbuf * (p + 1) / parts);
+        const uint32_t nb = b1 - b0;
+        const uint64_t byte0 = uniform_len ? (uint64_t)b0 * uniform_len : 0;
+        const uint8_t* data_p = d_data + byte0;
+        uint32_t* bitmap_p = e->bitmap.p + (byte0 >> 5);
+        uint32_t* small_p = e->small.p + (uint64_t)kSmall * p;
+        uint32_t* hist = small_p;
+        uint32_t* cursor = small_p + kMaxBins;
+        uint32_t* part_total = small_p + 2 * kMaxBins + 1;
+        const uint64_t slot0 = (uint64_t)b0 * out->cap;
 
-    ResolveArgs ra{};
-    ra.bitmap = e->bitmap.p;
-    ra.offs = d_offs;
-    ra.lens = d_lens;
-    ra.nbuf = nbuf;
-    ra.uniform_len = uniform_len;
-    ra.first_off = e->first_off;
-    ra.max_len = e->prm.max_len;
-    ra.cap = out->cap;
-    ra.bin_shift = e->bin_shift;
-    ra.nbins = e->nbins;
-    ra.counts = out->counts;
-    ra.starts = out->starts;
-    ra.clens = out->lens;
-    ra.hist = hist;
-    ra.overflow = overflow;
-    HIP_TRY(launch_resolve(ra, s));
-    if (timing) HIP_TRY(hipEventRecord(e->ev[3], s));
+        // ---- scan (s_scan)
+        ScanArgs sa{};
+        sa.data = data_p;
+        sa.offs = d_offs;
+        sa.lens = d_lens;
+        sa.bitmap = bitmap_p;
+        sa.nbuf = nb;
+        sa.uniform_len = uniform_len;
+        sa.seg_len = e->seg_len;
+        sa.jshift = (uint32_t)(e->degree - 40);
+        sa.mask_lo = (uint32_t)e->prm.pred_mask;
+        sa.mask_hi = (uint32_t)(e->prm.pred_mask >> 32);
+        sa.val_lo = (uint32_t)e->prm.pred_value;
+        sa.val_hi = (uint32_t)(e->prm.pred_value >> 32);
+        sa.tab_image = e->tab_image.p;
+        sa.zero_page = e->zero_page.p;
+        uint64_t seg_bound;
+        if (uniform_len) {
+            const uint64_t spb = (uniform_len + e->seg_len - 1) / e->seg_len;
+            sa.total_segs = spb * nb;
+            seg_bound = sa.total_segs;
+        } else {
+            sa.seg_prefix = e->seg_prefix.p;
+            seg_bound = data_bytes / e->seg_len + nb;
+        }
+        const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
+        uint64_t grid = (seg_bound + per_block - 1) / per_block;
+        grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus * e->scan_info.wg_per_cu);
+        grid = std::max<uint64_t>(grid, 1);
+        {
+            const int t = t_begin(e, K_SCAN, sscan);
+            HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, sscan));
+            t_end(e, t, sscan);
+        }
+        if (parts > 1) {
+            HIP_TRY(hipEventRecord(e->ev_scan[p], sscan));
+            HIP_TRY(hipStreamWaitEvent(spost, e->ev_scan[p], 0));
+        }
 
-    PrefixArgs pa{};
-    pa.counts = out->counts;
-    pa.nbuf = nbuf;
-    pa.hist = hist;
-    pa.nbins = e->nbins;
-    pa.cursor = cursor;
-    pa.rec_base = e->rec_base.p;
-    pa.total = out->total;
-    HIP_TRY(launch_prefix(pa, s));
-    if (timing) HIP_TRY(hipEventRecord(e->ev[4], s));
-
-    ScatterArgs ca{};
-    ca.counts = out->counts;
-    ca.clens = out->lens;
-    ca.nbuf = nbuf;
-    ca.cap = out->cap;
-    ca.bin_shift = e->bin_shift;
-    ca.nbins = e->nbins;
-    ca.cursor = cursor;
-    ca.tasks = e->tasks.p;
-    HIP_TRY(launch_scatter(ca, s));
-    if (timing) HIP_TRY(hipEventRecord(e->ev[5], s));
-
-    HashArgs ha{};
-    ha.data = d_data;
-    ha.offs = d_offs;
-    ha.uniform_len = uniform_len;
-    ha.tasks = e->tasks.p;
-    ha.total = out->total;
-    ha.starts = out->starts;
-    ha.clens = out->lens;
-    ha.rec_base = e->rec_base.p;
-    ha.cap = out->cap;
-    ha.digests = out->digests;
-    ha.records = out->records;
-    ha.records_cap = out->records_cap;
-    ha.buffer_id_base = buffer_id_base;
-    ha.algo = e->prm.hash_algo;
-    // upper bound on chunks: every buffer at most cap
-    HIP_TRY(launch_hash(ha, nslots, e->hash_variant, s));
-    if (timing) {
-        HIP_TRY(hipEventRecord(e->ev[6], s));
-        e->runs_recorded++;
+        // ---- resolve, prefix, scatter, hash (s_post)
+        ResolveArgs ra{};
+        ra.bitmap = bitmap_p;
+        ra.offs = d_offs;
+        ra.lens = d_lens;
+        ra.nbuf = nb;
+        ra.uniform_len = uniform_len;
+        ra.first_off = e->first_off;
+        ra.max_len = e->prm.max_len;
+        ra.cap = out->cap;
+        ra.bin_shift = e->bin_shift;
+        ra.nbins = e->nbins;
+        ra.counts = out->counts + b0;
+        ra.starts = out->starts + slot0;
+        ra.clens = out->lens + slot0;
+        ra.hist = hist;
+        ra.overflow = e->small.p + 2 * kMaxBins;  // part 0's word: one flag for the whole run
+        {
+            const int t = t_begin(e, K_RESOLVE, spost);
+            HIP_TRY(launch_resolve(ra, spost));
+            t_end(e, t, spost);
+        }
+        PrefixArgs pa{};
+        pa.counts = out->counts + b0;
+        pa.nbuf = nb;
+        pa.hist = hist;
+        pa.nbins = e->nbins;
+        pa.cursor = cursor;
+        pa.rec_base = e->rec_base.p + b0;
+        pa.total = part_total;
+        pa.base_in = p ? running + p : nullptr;
+        pa.base_out = running + p + 1;
+        pa.grand_total = p + 1 == parts ? out->total : nullptr;
+        {
+            const int t = t_begin(e, K_PREFIX, spost);
+            HIP_TRY(launch_prefix(pa, spost));
+            t_end(e, t, spost);
+        }
+        ScatterArgs ca{};
+        ca.counts = out->counts + b0;
+        ca.clens = out->lens + slot0;
+        ca.nbuf = nb;
+        ca.cap = out->cap;
+        ca.bin_shift = e->bin_shift;
+        ca.nbins = e->nbins;
+        ca.cursor = cursor;
+        ca.tasks = e->tasks.p + slot0;
+        {
+            const int t = t_begin(e, K_SCATTER, spost);
+            HIP_TRY(launch_scatter(ca, spost));
+            t_end(e, t, spost);
+        }
+        HashArgs ha{};
+        ha.data = data_p;
+        ha.offs = d_offs;
+        ha.uniform_len = uniform_len;
+        ha.tasks = e->tasks.p + slot0;
+        ha.total = part_total;
+        ha.starts = out->starts + slot0;
+        ha.clens = out->lens + slot0;
+        ha.rec_base = e->rec_base.p + b0;
+        ha.cap = out->cap;
+        ha.digests = out->digests + slot0 * 32;
+        ha.records = out->records;
+        ha.records_cap = out->records_cap;
+        ha.buffer_id_base = buffer_id_base + b0;
+        ha.algo = e->prm.hash_algo;
+        {
+            const int t = t_begin(e, K_HASH, spost);
+            HIP_TRY(launch_hash(ha, (uint64_t)nb * out->cap, e->hash_variant, spost));
+            t_end(e, t, spost);
+        }
     }
+    if (parts > 1) {
+        HIP_TRY(hipEventRecord(e->ev_done, spost));
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_done, 0));
+    }
+    t_end(e, tpipe, s);
+    if (e->run) e->runs_recorded++;
     return SDFS_CDC_OK;
 }
 
@@ -375,7 +470,7 @@ int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, co
         HIP_TRY(hipMemcpyAsync(pl, out.lens, nout * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(pd, out.digests, nout * 32, hipMemcpyDeviceToHost, s));
         uint32_t ovf = 0;
-        HIP_TRY(hipMemcpyAsync(&ovf, e->small.p + 2 * kMaxBins, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&ovf, e->small.p + 2 * kMaxBins, 4, hipMemcpyDeviceToHost, s));  // run-wide flag
         HIP_TRY(hipStreamSynchronize(s));
         if (ovf) return fail(SDFS_CDC_EHIP, "internal: chunk slot overflow");
         for (uint32_t i = 0; i < n; i++) {
@@ -443,10 +538,20 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     e->bin_shift = 0;
     while ((maxblocks >> e->bin_shift) >= (uint32_t)kMaxBins) e->bin_shift++;
     e->nbins = (maxblocks >> e->bin_shift) + 1;
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete e;
-        return fail(SDFS_CDC_EHIP, "hipStreamCreate failed");
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->s_scan, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->s_post, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_done, hipEventDisableTiming) != hipSuccess) {
+        sdfs_cdc_destroy(e);
+        return fail(SDFS_CDC_EHIP, "stream/event creation failed");
     }
+    for (auto& ev : e->ev_scan)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            sdfs_cdc_destroy(e);
+            return fail(SDFS_CDC_EHIP, "event creation failed");
+        }
+    if (const char* v = getenv("SDFS_PIPE_PARTS")) e->parts = std::max(1, std::min(atoi(v), kMaxParts));
     // tuning overrides for experiments (DESIGN.md "Scan variants"); production uses variant 0
     if (const char* v = getenv("SDFS_SCAN_VARIANT")) e->scan_variant = atoi(v);
     if (const char* v = getenv("SDFS_SEG_LEN")) e->seg_len = (uint32_t)atoi(v);
@@ -490,10 +595,18 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
         e->o_digests.release();
         if (e->pin_data) (void)hipHostFree(e->pin_data);
         if (e->pin_out) (void)hipHostFree(e->pin_out);
+        if (e->s_scan) (void)hipStreamSynchronize(e->s_scan);
+        if (e->s_post) (void)hipStreamSynchronize(e->s_post);
         for (auto& run : e->ev_runs)
-            for (auto& ev : run)
+            for (auto& ev : run.ev)
                 if (ev) (void)hipEventDestroy(ev);
+        for (auto& ev : e->ev_scan)
+            if (ev) (void)hipEventDestroy(ev);
+        if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+        if (e->ev_done) (void)hipEventDestroy(e->ev_done);
         if (e->stream) (void)hipStreamDestroy(e->stream);
+        if (e->s_scan) (void)hipStreamDestroy(e->s_scan);
+        if (e->s_post) (void)hipStreamDestroy(e->s_post);
     }
     delete e;
     return SDFS_CDC_OK;
@@ -534,9 +647,10 @@ int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns) {
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
     while ((int)e->ev_runs.size() < nruns) {
-        std::vector<hipEvent_t> run(kNumTimed + 1, nullptr);
-        for (auto& ev : run) HIP_TRY(hipEventCreate(&ev));
-        e->ev_runs.push_back(std::move(run));
+        sdfs_cdc_engine::TimedRun r;
+        r.ev.assign(kEvPerRun, nullptr);
+        for (auto& ev : r.ev) HIP_TRY(hipEventCreate(&ev));
+        e->ev_runs.push_back(std::move(r));
     }
     e->timing_slots = nruns;
     e->runs_recorded = 0;
@@ -549,20 +663,31 @@ int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int
     HIP_TRY(hipSetDevice(e->prm.device));
     if (e->timing_slots == 0 || e->runs_recorded == 0) return 0;
     const uint64_t nr = std::min<uint64_t>(e->runs_recorded, (uint64_t)e->timing_slots);
+    double sum[kNumTimed] = {};
+    for (uint64_t r = 0; r < nr; r++) {
+        auto& run = e->ev_runs[(e->runs_recorded - 1 - r) % e->timing_slots];
+        for (size_t i = 0; i < run.kid.size(); i++) {
+            HIP_TRY(hipEventSynchronize(run.ev[2 * i + 1]));
+            float t = 0;
+            HIP_TRY(hipEventElapsedTime(&t, run.ev[2 * i], run.ev[2 * i + 1]));
+            sum[run.kid[i]] += t;
+        }
+    }
     int k = 0;
     for (int i = 0; i < kNumTimed && k < n; i++, k++) {
-        double sum = 0;
-        for (uint64_t r = 0; r < nr; r++) {
-            auto& run = e->ev_runs[(e->runs_recorded - 1 - r) % e->timing_slots];
-            HIP_TRY(hipEventSynchronize(run[i + 1]));
-            float t = 0;
-            HIP_TRY(hipEventElapsedTime(&t, run[i], run[i + 1]));
-            sum += t;
-        }
         if (names) names[k] = kKernelNames[i];
-        if (ms) ms[k] = (float)(sum / nr);
+        if (ms) ms[k] = (float)(sum[i] / nr);
     }
     return k;
+}
+
+int sdfs_cdc_set_pipeline(sdfs_cdc_engine* e, int parts, uint64_t part_min_bytes) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    if (parts < 1 || parts > kMaxParts) return fail(SDFS_CDC_EINVAL, "parts %d outside [1,%d]", parts, kMaxParts);
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->parts = parts;
+    e->part_min_bytes = part_min_bytes;
+    return SDFS_CDC_OK;
 }
 
 int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,

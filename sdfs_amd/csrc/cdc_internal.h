@@ -68,8 +68,11 @@ struct PrefixArgs {
     const uint32_t* hist;
     uint32_t nbins;
     uint32_t* cursor;     // [nbins] exclusive prefix, descending bin order
-    uint32_t* rec_base;   // [nbuf] exclusive prefix of counts
-    uint32_t* total;      // [1]
+    uint32_t* rec_base;   // [nbuf] exclusive prefix of counts (+ *base_in)
+    uint32_t* total;      // [1] chunks of this (sub-)batch
+    const uint32_t* base_in;  // nullable: records of the earlier sub-batches
+    uint32_t* base_out;       // nullable: *base_in + total
+    uint32_t* grand_total;    // nullable: same as base_out, the caller's total
 };
 
 struct ScatterArgs {

@@ -591,13 +591,18 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(PrefixArgs a) {
         part[t] += v;
         __syncthreads();
     }
-    uint32_t run = part[t] - sum;
+    const uint32_t base = a.base_in ? *a.base_in : 0u;
+    uint32_t run = base + part[t] - sum;
     if (a.rec_base)
         for (uint32_t b = b0; b < b1; b++) {
             a.rec_base[b] = run;
             run += a.counts[b];
         }
-    if (t == 1023) *a.total = part[1023];
+    if (t == 1023) {
+        *a.total = part[1023];
+        if (a.base_out) *a.base_out = base + part[1023];
+        if (a.grand_total) *a.grand_total = base + part[1023];
+    }
 }
 
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s) {

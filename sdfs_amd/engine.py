@@ -248,6 +248,10 @@ class HipVariableSha256HashEngine:
     def sync(self) -> None:
         check(self._lib.sdfs_cdc_stream_sync(self._h))
 
+    def set_pipeline(self, parts: int, part_min_bytes: int = 512 << 20) -> None:
+        """Sub-batch pipelining of run_device (scan of part k+1 overlaps hash of part k)."""
+        check(self._lib.sdfs_cdc_set_pipeline(self._h, int(parts), int(part_min_bytes)))
+
     def set_timing(self, nruns: int) -> None:
         """Record HIP events around every kernel of the next runs (ring of `nruns`; 0 = off)."""
         check(self._lib.sdfs_cdc_set_timing(self._h, int(nruns)))

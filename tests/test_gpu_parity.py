@@ -224,6 +224,30 @@ def test_device_b1_full_size_properties():
     assert 7000 < mean < 9500, mean  # ~8.2 KiB for a 12-bit predicate, min 4095
 
 
+@pytest.mark.parametrize("parts", [1, 3, 7])
+def test_device_subbatch_pipeline_matches(parts):
+    """Sub-batch pipelining (scan of part k+1 on one stream, hash of part k on another) gives the
+    same slots, totals and record table as one part, and matches the oracle."""
+    prm = P()
+    e = HipVariableSha256HashEngine(config=SdfsConfig())
+    e.set_pipeline(parts, 1 << 20)
+    batch = DeviceBatch(e, nbuf=300, buf_len=262144)
+    batch.fill_streams(first_stream=200, bufs_per_stream=100)
+    for _ in range(2):  # back-to-back runs on the same stream
+        batch.run(buffer_id_base=7)
+    counts, st, ln, dg, total = batch.host_results()
+    _check_cover(counts, st, ln, 262144, prm)
+    _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 100, 200, [0, 1, 99, 100, 101, 150, 199, 200, 298, 299])
+    rec = batch.record_table().cpu().numpy()
+    assert rec.shape[0] == total == int(counts.sum())
+    base = np.concatenate([[0], np.cumsum(counts.astype(np.int64))[:-1]]).astype(np.int64)
+    for b in (0, 99, 100, 150, 299):
+        for i in range(counts[b]):
+            r = rec[base[b] + i]
+            assert bytes(r[:32]) == bytes(dg[b, i]) and int.from_bytes(bytes(r[32:40]), "little") == 7 + b
+    e.destroy()
+
+
 def test_device_dedup_50pct_copies_are_identical():
     """configs[2] shape: half the buffers are byte copies of earlier fresh ones (dedup-hit path)."""
     e = engine_for(P())
