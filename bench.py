@@ -148,7 +148,8 @@ def main():
     dom = max(("cdc_scan", "chunk_hash"), key=lambda k: kt.get(k, 0.0))
     t_dom = kt.get(dom, 0.0) / 1e3
     achieved = nbytes / t_dom / 1e9 if t_dom > 0 else 0.0
-    dev_ms = sum(v for k, v in kt.items())
+    # device time of one pass: the pipeline-level events when present, else the stage sum
+    dev_ms = kt.get("pipeline") or sum(v for k, v in kt.items() if k != "pipeline")
     valu = {k: round(nbytes * OPS_PER_BYTE[k] / (kt[k] / 1e3) / VALU_PEAK_OPS, 3) for k in OPS_PER_BYTE if kt.get(k)}
     cpu = None
     if world == 1 and args.cpu_secs > 0:
