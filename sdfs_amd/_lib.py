@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # SDFS_CDC_LIB selects an alternative in-tree build (kernel-variant sweeps, scripts/sweep_scan.py)
 LIB_PATH = os.environ.get("SDFS_CDC_LIB") or os.path.join(HERE, "libsdfs_cdc.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "sdfs_cdc.h")
+HEADER_PATHS = [HEADER_PATH, os.path.join(os.path.dirname(HERE), "include", "sdfs_index.h")]
 
 OK, EINVAL, ECAP, EHIP, ENOMEM, ENODEV = 0, -1, -2, -3, -4, -5
 SHA256, SHA256_160, MD5 = 0, 1, 2
@@ -91,6 +92,13 @@ SIGNATURES = {
     "sdfs_cdc_kernel_times": (ctypes.c_int, [_vp, _P(ctypes.c_char_p), _P(ctypes.c_float), ctypes.c_int]),
     "sdfs_cdc_synth_device": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                              ctypes.c_uint64, _vp]),
+    # include/sdfs_index.h
+    "sdfs_cdc_index_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _P(_vp)]),
+    "sdfs_cdc_index_destroy": (ctypes.c_int, [_vp]),
+    "sdfs_cdc_index_put_records": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, _vp,
+                                                  _vp, _vp]),
+    "sdfs_cdc_index_get": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
+    "sdfs_cdc_index_size": (ctypes.c_int, [_vp, _u64p, _u64p]),
 }
 
 _lib = None

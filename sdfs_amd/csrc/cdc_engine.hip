@@ -33,6 +33,21 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+// shared with the other C-ABI translation units (dedup_index.hip)
+int sdfs::fail_status(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+namespace {
+
 #define HIP_TRY(expr)                                                                             \
     do {                                                                                          \
         hipError_t _e = (expr);                                                                   \
@@ -111,6 +126,7 @@ struct sdfs_cdc_engine {
     uint32_t seg_len = 4096;  // bytes of one buffer per lane (multiple of the variant's block)
     int scan_variant = 0;
     int hash_variant = 0;
+    int hash_wg_per_cu = 2;  // persistent hash variant: 256-thread workgroups per CU
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
@@ -308,21 +324,6 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
             sa.seg_prefix = e->seg_prefix.p;
             seg_bound = data_bytes / e->seg_len + nb;
         }
-        const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
-        uint64_t grid = (seg_bound + per_block - 1) / per_block;
-        grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus * e->scan_info.wg_per_cu);
-        grid = std::max<uint64_t>(grid, 1);
-        {
-            const int t = t_begin(e, K_SCAN, sscan);
-            HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, sscan));
-            t_end(e, t, sscan);
-        }
-        if (parts > 1) {
-            HIP_TRY(hipEventRecord(e->ev_scan[p], sscan));
-            HIP_TRY(hipStreamWaitEvent(spost, e->ev_scan[p], 0));
-        }
-
-        // ---- resolve, prefix, scatter, hash (s_post)
         ResolveArgs ra{};
         ra.bitmap = bitmap_p;
         ra.offs = d_offs;
@@ -339,7 +340,28 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
         ra.clens = out->lens + slot0;
         ra.hist = hist;
         ra.overflow = e->small.p + 2 * kMaxBins;  // part 0's word: one flag for the whole run
+        // one wave = one buffer: the fused scan variant resolves inside the scan kernel
+        // (single stream only: the histogram it feeds is cleared on the post stream)
+        const bool fused = e->scan_info.fuse && parts == 1 && uniform_len && e->scan_info.chains == 1 &&
+                           (uint64_t)uniform_len == 64ull * e->seg_len;
+        sa.fuse_resolve = fused ? 1u : 0u;
+        sa.res = ra;
+        const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
+        uint64_t grid = (seg_bound + per_block - 1) / per_block;
+        grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus * e->scan_info.wg_per_cu);
+        grid = std::max<uint64_t>(grid, 1);
         {
+            const int t = t_begin(e, K_SCAN, sscan);
+            HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, sscan));
+            t_end(e, t, sscan);
+        }
+        if (parts > 1) {
+            HIP_TRY(hipEventRecord(e->ev_scan[p], sscan));
+            HIP_TRY(hipStreamWaitEvent(spost, e->ev_scan[p], 0));
+        }
+
+        // ---- resolve, prefix, scatter, hash (s_post)
+        if (!fused) {
             const int t = t_begin(e, K_RESOLVE, spost);
             HIP_TRY(launch_resolve(ra, spost));
             t_end(e, t, spost);
@@ -389,6 +411,8 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
         ha.records_cap = out->records_cap;
         ha.buffer_id_base = buffer_id_base + b0;
         ha.algo = e->prm.hash_algo;
+        ha.wave_ctr = small_p + 2 * kMaxBins + 2;  // zeroed with the rest of `small` above
+        ha.persist_grid = (uint32_t)(e->num_cus * e->hash_wg_per_cu);
         {
             const int t = t_begin(e, K_HASH, spost);
             HIP_TRY(launch_hash(ha, (uint64_t)nb * out->cap, e->hash_variant, spost));
@@ -556,6 +580,7 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     if (const char* v = getenv("SDFS_SCAN_VARIANT")) e->scan_variant = atoi(v);
     if (const char* v = getenv("SDFS_SEG_LEN")) e->seg_len = (uint32_t)atoi(v);
     if (const char* v = getenv("SDFS_HASH_VARIANT")) e->hash_variant = atoi(v);
+    if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
     e->scan_info = scan_variant_info(e->scan_variant);
     if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0) {
         sdfs_cdc_destroy(e);

@@ -22,27 +22,13 @@ struct ScanVariantInfo {
     int lds_bytes;   // LDS image size
     int wg_per_cu;   // resident workgroups per CU the variant is built for
     int blk;         // bytes per lane per iteration (segment length must be a multiple)
+    int fuse;        // resolves cuts in the epilogue when one wave = one buffer (sweep-only:
+                     // measured slower)
 };
 ScanVariantInfo scan_variant_info(int variant);
 
 constexpr int kMaxBins = 512;  // SHA work binning by block count (DESIGN.md "Load balance")
 constexpr int kRecordBytes = 48;
-
-struct ScanArgs {
-    const uint8_t* data;
-    const uint64_t* offs;        // general layout (nullptr when uniform)
-    const uint32_t* lens;
-    const uint64_t* seg_prefix;  // [nbuf+1] segment prefix (general layout)
-    uint32_t* bitmap;            // 1 bit per byte position, bit i of word w = position 32w+i
-    uint64_t total_segs;
-    uint32_t nbuf;
-    uint32_t uniform_len;        // != 0 -> uniform layout
-    uint32_t seg_len;            // bytes per segment, multiple of 64
-    uint32_t jshift;             // deg(P) - 40 : bit offset of the push index inside the hi word
-    uint32_t mask_lo, mask_hi, val_lo, val_hi;
-    const uint8_t* tab_image;    // global copy of the LDS image (scan_lds_bytes(copies))
-    const uint8_t* zero_page;    // 256 zero bytes (branch-free prefetch of tail blocks)
-};
 
 struct ResolveArgs {
     const uint32_t* bitmap;
@@ -61,6 +47,28 @@ struct ResolveArgs {
     uint32_t* hist;      // [nbins]
     uint32_t* overflow;  // [1] set when a buffer needs more than cap slots
 };
+
+struct ScanArgs {
+    const uint8_t* data;
+    const uint64_t* offs;        // general layout (nullptr when uniform)
+    const uint32_t* lens;
+    const uint64_t* seg_prefix;  // [nbuf+1] segment prefix (general layout)
+    uint32_t* bitmap;            // 1 bit per byte position, bit i of word w = position 32w+i
+    uint64_t total_segs;
+    uint32_t nbuf;
+    uint32_t uniform_len;        // != 0 -> uniform layout
+    uint32_t seg_len;            // bytes per segment, multiple of 64
+    uint32_t jshift;             // deg(P) - 40 : bit offset of the push index inside the hi word
+    uint32_t mask_lo, mask_hi, val_lo, val_hi;
+    const uint8_t* tab_image;    // global copy of the LDS image (scan_lds_bytes(copies))
+    const uint8_t* zero_page;    // 256 zero bytes (branch-free prefetch of tail blocks)
+    // fused cut resolution: when every wave's 64 segments are exactly one buffer (uniform layout,
+    // uniform_len == 64 * seg_len, one segment per lane), the wave resolves that buffer's cuts
+    // right after scanning it, from its own L2-resident bitmap words (no separate resolve pass)
+    uint32_t fuse_resolve;
+    ResolveArgs res;
+};
+
 
 struct PrefixArgs {
     const uint32_t* counts;
@@ -101,7 +109,12 @@ struct HashArgs {
     uint64_t records_cap;
     uint64_t buffer_id_base;
     uint32_t algo;             // SDFS_CDC_SHA256 / _SHA256_160 / _MD5
+    uint32_t persist_grid;     // workgroups of the persistent variant (0 = not used)
+    uint32_t* wave_ctr;        // [1] zeroed task counter of the persistent variant
 };
+
+// Record a C-ABI error message (sdfs_cdc_last_error) and return `code`.
+int fail_status(int code, const char* fmt, ...);
 
 inline uint64_t splitmix64_host(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;

@@ -1,5 +1,5 @@
 """CPU tests of the drop-in boundary: the HIP library loads, exports every entry point that
-include/sdfs_cdc.h declares, the Python mirror binds them all, and the product path fails loudly
+include/sdfs_cdc.h and include/sdfs_index.h declare, the Python mirror binds them all, and the product path fails loudly
 (no CPU fallback) when there is no gfx950 device.  No compute calls without a GPU."""
 import ctypes
 import os
@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    hdr = open(_lib.HEADER_PATH).read()
+    hdr = "".join(open(h).read() for h in _lib.HEADER_PATHS)
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
     return sorted(set(re.findall(r"\b(sdfs_cdc_\w+)\s*\(", hdr)))
 
