@@ -12,7 +12,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # SDFS_CDC_LIB selects an alternative in-tree build (kernel-variant sweeps, scripts/sweep_scan.py)
-LIB_PATH = os.environ.get("SDFS_CDC_LIB") or os.path.join(HERE, "libsdfs_cdc.so")
+DEFAULT_LIB = os.path.join(HERE, "libsdfs_cdc.so")
+LIB_PATH = os.environ.get("SDFS_CDC_LIB") or DEFAULT_LIB
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "sdfs_cdc.h")
 HEADER_PATHS = [HEADER_PATH, os.path.join(os.path.dirname(HERE), "include", "sdfs_index.h")]
 
@@ -112,7 +113,11 @@ def load():
             raise ImportError(f"{LIB_PATH} not built: run `make` or __graft_entry__.build()")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                if LIB_PATH == DEFAULT_LIB:
+                    raise ImportError(f"{LIB_PATH} does not export {name}: rebuild it")
+                continue  # an older build selected for an A/B measurement
             fn.restype = res
             fn.argtypes = args
         _lib = lib

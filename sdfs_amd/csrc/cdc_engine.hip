@@ -142,6 +142,7 @@ struct sdfs_cdc_engine {
     DevBuf<uint32_t> small;  // hist[kMaxBins] | cursor[kMaxBins] | overflow[1]
     DevBuf<uint32_t> rec_base;
     DevBuf<uint32_t> tasks;
+    DevBuf<uint32_t> spec_starts, spec_cnt, spec_next;  // sectioned cut walk of very long buffers
     // host-path device buffers
     DevBuf<uint8_t> h_data;
     DevBuf<uint64_t> h_offs;
@@ -227,7 +228,7 @@ void t_end(sdfs_cdc_engine* e, int i, hipStream_t st) {
 // the VALU-bound hash share the CUs (DESIGN.md "Pipeline").  Caller holds e->mu.
 int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
                  const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
-                 const sdfs_cdc_dev_out* out, hipStream_t s) {
+                 const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len = 0) {
     if (!out || !out->counts || !out->starts || !out->lens || !out->digests || !out->total)
         return fail(SDFS_CDC_EINVAL, "incomplete sdfs_cdc_dev_out");
     if (uniform_len && (uniform_len & 63)) return fail(SDFS_CDC_EINVAL, "uniform_len must be a multiple of 64");
@@ -340,6 +341,19 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
         ra.clens = out->lens + slot0;
         ra.hist = hist;
         ra.overflow = e->small.p + 2 * kMaxBins;  // part 0's word: one flag for the whole run
+        ra.max_buf_len = uniform_len ? uniform_len : max_buf_len;
+        ra.sec_len = resolve_section_len(ra.max_buf_len, e->prm.max_len);
+        if (ra.sec_len) {
+            ra.nsec = (uint32_t)((ra.max_buf_len + ra.sec_len - 1) / ra.sec_len);
+            ra.spec_cap = ra.sec_len / (e->first_off + 1) + 2;
+            const uint64_t items = (uint64_t)nb * ra.nsec;
+            HIP_TRY(e->spec_starts.ensure(items * ra.spec_cap));
+            HIP_TRY(e->spec_cnt.ensure(items));
+            HIP_TRY(e->spec_next.ensure(items));
+            ra.spec_starts = e->spec_starts.p;
+            ra.spec_cnt = e->spec_cnt.p;
+            ra.spec_next = e->spec_next.p;
+        }
         // one wave = one buffer: the fused scan variant resolves inside the scan kernel
         // (single stream only: the histogram it feeds is cleared on the post stream)
         const bool fused = e->scan_info.fuse && parts == 1 && uniform_len && e->scan_info.chains == 1 &&
@@ -478,7 +492,7 @@ int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, co
         out.digests = e->o_digests.p;
         out.cap = dcap;
         out.total = e->o_total.p;
-        rc = run_pipeline(e, e->h_data.p, bytes, e->h_offs.p, e->h_lens.p, n, 0, 0, &out, s);
+        rc = run_pipeline(e, e->h_data.p, bytes, e->h_offs.p, e->h_lens.p, n, 0, 0, &out, s, maxlen);
         if (rc) return rc;
         // results back through pinned memory
         const uint64_t nout = (uint64_t)n * dcap;
@@ -610,6 +624,9 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
         e->small.release();
         e->rec_base.release();
         e->tasks.release();
+        e->spec_starts.release();
+        e->spec_cnt.release();
+        e->spec_next.release();
         e->h_data.release();
         e->h_offs.release();
         e->h_lens.release();
@@ -663,7 +680,10 @@ int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-    return run_pipeline(e, d_data, data_bytes, d_offs, d_lens, nbuf, 0, buffer_id_base, out, s);
+    // the longest buffer is not known on the host: a few buffers sharing data_bytes are treated as
+    // long (LDS-staged cut walk), many as their mean length
+    const uint64_t max_len_hint = nbuf <= 4u * (uint32_t)e->num_cus ? data_bytes : data_bytes / (nbuf ? nbuf : 1);
+    return run_pipeline(e, d_data, data_bytes, d_offs, d_lens, nbuf, 0, buffer_id_base, out, s, max_len_hint);
 }
 
 int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns) {

@@ -46,7 +46,17 @@ struct ResolveArgs {
     uint32_t* clens;
     uint32_t* hist;      // [nbins]
     uint32_t* overflow;  // [1] set when a buffer needs more than cap slots
+    uint64_t max_buf_len;  // longest buffer of a ragged batch (selects the resolve kernel)
+    // sectioned walk of long buffers (speculate per section, then stitch; engine scratch)
+    uint32_t sec_len;      // positions per section (0 = not sectioned)
+    uint32_t nsec;         // sections per buffer (of the longest buffer)
+    uint32_t spec_cap;     // chunk starts recorded per section
+    uint32_t* spec_starts; // [nbuf * nsec * spec_cap]
+    uint32_t* spec_cnt;    // [nbuf * nsec]
+    uint32_t* spec_next;   // [nbuf * nsec] first chunk start at or past the section end
 };
+// Section length of the sectioned cut walk for a buffer of `len` bytes (0 = not sectioned).
+uint32_t resolve_section_len(uint64_t len, uint32_t max_len);
 
 struct ScanArgs {
     const uint8_t* data;

@@ -2,7 +2,8 @@
 //
 // Pipeline per batch of write buffers (DESIGN.md "Kernels"):
 //   1. cdc_scan     windowed Rabin rolling hash over every byte -> candidate bitmap (1 bit/byte)
-//   2. cdc_resolve  greedy cut resolution per buffer (min/max rules) -> (start,len) slots
+//   2. cdc_resolve  greedy cut resolution per buffer (min/max rules) -> (start,len) slots;
+//                   long buffers: LDS-staged walk, very long ones: speculative sections + stitch
 //   3. cdc_prefix   bin cursors (longest-first) + per-buffer record bases + total
 //   4. cdc_scatter  chunk slots -> task list sorted by SHA block count (load balance)
 //   5. chunk_hash   one lane per chunk: SHA-256 / MD5 over the chunk bytes -> digests, records
@@ -10,6 +11,8 @@
 // Reference semantics: VariableSha256HashEngine.getChunks (VariableSha256HashEngine.java:71-86)
 // driving the rabinwindow EnhancedFingerFactory loop; getHash (:58-67).
 // Integer/bit work only: no MFMA (DESIGN.md explains the VALU roofline).
+#include <algorithm>
+
 #include "cdc_internal.h"
 
 namespace sdfs {
@@ -229,6 +232,42 @@ __device__ __forceinline__ int64_t find_first(const uint32_t* bm, uint64_t word0
     return -1;
 }
 
+// First candidate in [lo, hi] from the global bitmap, each lane testing 8 consecutive words
+// (a wave covers 16 Ki positions per coalesced 2 KiB load).
+__device__ __forceinline__ int64_t find_first_wide(const uint32_t* bm, uint64_t word0, uint32_t lo, uint32_t hi,
+                                                   uint32_t lane) {
+    const uint32_t lo_w = lo >> 5, hi_w = hi >> 5, lo_b = lo & 31, hi_b = hi & 31;
+    for (uint32_t wb = lo_w; wb <= hi_w; wb += 512) {
+        const uint32_t w0 = wb + 8 * lane;
+        uint32_t bits[8];
+        uint32_t any = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t w = w0 + j;
+            uint32_t v = 0;
+            if (w <= hi_w) {
+                v = bm[word0 + w];
+                if (w == lo_w) v &= ~0u << lo_b;
+                if (w == hi_w) v &= hi_b == 31 ? ~0u : ((2u << hi_b) - 1u);
+            }
+            bits[j] = v;
+            any |= v;
+        }
+        const uint64_t m = __ballot(any != 0);
+        if (m) {
+            const uint32_t l = __builtin_ctzll(m);
+            uint32_t jj = 0, bb = 0;
+#pragma unroll
+            for (int j = 7; j >= 0; j--)
+                if (bits[j]) { jj = j; bb = bits[j]; }
+            const uint32_t pos_in = jj * 32 + (bb ? __builtin_ctz(bb) : 0);
+            const uint32_t p = __shfl(pos_in, l);
+            return (int64_t)(wb + 8 * l) * 32 + p;
+        }
+    }
+    return -1;
+}
+
 __device__ __forceinline__ uint32_t sha_blocks(uint32_t len) { return (len + 8) / 64 + 1; }
 
 // Greedy cut walk over one buffer's candidate bits (one wave, wave-uniform control flow):
@@ -245,6 +284,8 @@ __device__ __forceinline__ void resolve_buffer(const ResolveArgs& a, uint32_t b,
             const uint64_t forced = start + a.max_len - 1;
             const uint64_t hi = forced < len - 1 ? forced : len - 1;
             int64_t k = -1;
+            // 64 words per probe: with thousands of short buffers this kernel is throughput-bound and
+            // the 8-word-per-lane search (find_first_wide) measured 2.5x slower here
             if (lo <= hi) k = find_first(a.bitmap, word0, lo, hi, lane);
             if (k < 0) k = (int64_t)hi;  // forced cut at max_len, or the tail chunk
             const uint32_t clen = (uint32_t)(k + 1 - start);
@@ -581,7 +622,311 @@ __global__ __launch_bounds__(256) void cdc_resolve_kernel(ResolveArgs a) {
         if (lhist[i]) atomicAdd(&a.hist[i], lhist[i]);
 }
 
+// LDS-staged cut walk for long buffers (the BACKUP_VOLUME profile's 40 MiB write buffers).
+// One 256-thread workgroup per buffer.  Window n holds bitmap words [n*kResStride,
+// n*kResStride + 2*kResStride) of the buffer in one of two LDS slots; wave 0 walks the cuts of
+// window n from LDS (each lane tests 8 consecutive words, so one ballot covers 16 Ki positions:
+// about one iteration per chunk at a 4 KiB candidate spacing) while waves 1-3 stage window n+1
+// into the other slot.  The walk leaves window n at the first chunk whose search range ends past
+// it; with kResStride > max_len/32 + 1 words that range lies inside window n+1 (its start is at
+// least max_len before its end, its end at most max_len past window n's end), so the window
+// schedule is fixed and the staging never waits on the walk.
+constexpr uint32_t kResStride = 6144;          // words (196 608 positions)
+constexpr uint32_t kResWin = 2 * kResStride;   // words per window (48 KiB of LDS)
+constexpr uint32_t kResStage = kResWin / 2 / 192;  // uint2 loads per staging thread (waves 1-3)
+
+__device__ __forceinline__ int64_t find_first_lds(const uint32_t* win, uint32_t wbase, uint32_t lo_w, uint32_t lo_b,
+                                                  uint32_t hi_w, uint32_t hi_b, uint32_t lane) {
+    // words are buffer-relative; win[w - wbase]
+    for (uint32_t wb = lo_w; wb <= hi_w; wb += 512) {
+        const uint32_t w0 = wb + 8 * lane;
+        uint32_t bits[8];
+        uint32_t any = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t w = w0 + j;
+            uint32_t v = 0;
+            if (w <= hi_w) {
+                v = win[w - wbase];
+                if (w == lo_w) v &= ~0u << lo_b;
+                if (w == hi_w) v &= hi_b == 31 ? ~0u : ((2u << hi_b) - 1u);
+            }
+            bits[j] = v;
+            any |= v;
+        }
+        const uint64_t m = __ballot(any != 0);
+        if (m) {
+            const uint32_t l = __builtin_ctzll(m);
+            uint32_t jj = 0, bb = 0;
+#pragma unroll
+            for (int j = 7; j >= 0; j--)
+                if (bits[j]) { jj = j; bb = bits[j]; }
+            const uint32_t pos_in = jj * 32 + (bb ? __builtin_ctz(bb) : 0);
+            const uint32_t p = __shfl(pos_in, l);
+            return (int64_t)(wb + 8 * l) * 32 + p;
+        }
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void stage_window(uint32_t* slot, const uint32_t* bm, uint64_t word0, uint64_t wbase,
+                                             uint64_t nwords, uint32_t t, uint32_t nthreads_div) {
+    // thread t of the staging group loads kResWin/2/nthreads_div uint2 (all issued before any store)
+    const uint2* src = reinterpret_cast<const uint2*>(bm + word0 + wbase);
+    uint2* dst = reinterpret_cast<uint2*>(slot);
+    const uint64_t avail = nwords > wbase ? nwords - wbase : 0;
+    uint2 v[kResStage];
+#pragma unroll
+    for (uint32_t k = 0; k < kResStage; k++) {
+        const uint32_t i = t + k * nthreads_div;
+        v[k] = 2ull * i < avail ? src[i] : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kResStage; k++) dst[t + k * nthreads_div] = v[k];
+}
+
+// SPEC = false: item = buffer, the walk covers the whole buffer and writes the final chunk slots.
+// SPEC = true: item = (buffer, section); the walk starts a chunk at the section start, runs until
+// the next chunk start reaches the section end and records the starts for the stitch pass.
+template <bool SPEC>
+__global__ __launch_bounds__(256) void cdc_resolve_lds_kernel(ResolveArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t win[2][kResWin];
+    __shared__ uint32_t lhist[SPEC ? 1 : kMaxBins];
+    __shared__ uint32_t s_done[2];  // by window parity: the walker may write window n+1's flag
+                                    // before every thread has read window n's
+    if constexpr (!SPEC)
+        for (uint32_t i = threadIdx.x; i < a.nbins; i += 256) lhist[i] = 0;
+    const uint32_t lane = threadIdx.x & 63;
+    const bool walker = threadIdx.x < 64;
+    const uint32_t nitems = SPEC ? a.nbuf * a.nsec : a.nbuf;
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const uint32_t b = SPEC ? item / a.nsec : item;
+        const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
+        const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
+        const uint32_t r0 = SPEC ? (item - b * a.nsec) * a.sec_len : 0;
+        if (r0 >= len) {  // workgroup-uniform: section past this buffer's end
+            if constexpr (SPEC) {
+                if (threadIdx.x == 0) {
+                    a.spec_cnt[item] = 0;
+                    a.spec_next[item] = len;
+                }
+            }
+            continue;
+        }
+        const uint32_t r1 = SPEC ? min(r0 + a.sec_len, len) : len;
+        const uint64_t word0 = off >> 5;  // even: buffers start 64-byte aligned
+        const uint64_t nwords = ((uint64_t)len + 31) >> 5;
+        const uint32_t wb0 = (r0 >> 5) & ~1u;
+        uint32_t start = r0;  // walker state (wave 0 registers)
+        uint32_t cnt = 0;
+        __syncthreads();  // the previous item's walk is done with both slots
+        if (threadIdx.x >= 64) stage_window(win[0], a.bitmap, word0, wb0, nwords, threadIdx.x - 64, 192);
+        __syncthreads();
+        for (uint32_t n = 0;; n++) {
+            const uint32_t wbase = wb0 + n * kResStride;
+            if (!walker) {
+                stage_window(win[(n + 1) & 1], a.bitmap, word0, (uint64_t)wbase + kResStride, nwords,
+                             threadIdx.x - 64, 192);
+            } else {
+                const uint32_t* w = win[n & 1];
+                const uint64_t wend = (uint64_t)wbase + kResWin;  // first word past the window
+                while (start < r1) {
+                    const uint32_t lo = start + a.first_off;
+                    const uint32_t forced = start + a.max_len - 1;
+                    const uint32_t hi = forced < len - 1 ? forced : len - 1;
+                    if (lo <= hi && (uint64_t)(hi >> 5) >= wend) break;  // continues in window n+1
+                    int64_t k = -1;
+                    if (lo <= hi) k = find_first_lds(w, wbase, lo >> 5, lo & 31, hi >> 5, hi & 31, lane);
+                    if (k < 0) k = (int64_t)hi;
+                    if constexpr (SPEC) {
+                        if (lane == 0 && cnt < a.spec_cap) a.spec_starts[(uint64_t)item * a.spec_cap + cnt] = start;
+                    } else {
+                        const uint32_t clen = (uint32_t)k + 1 - start;
+                        if (cnt < a.cap) {
+                            if (lane == 0) {
+                                const uint64_t slot = (uint64_t)b * a.cap + cnt;
+                                a.starts[slot] = start;
+                                a.clens[slot] = clen;
+                                uint32_t bin = sha_blocks(clen) >> a.bin_shift;
+                                bin = bin < a.nbins ? bin : a.nbins - 1;
+                                atomicAdd(&lhist[bin], 1u);
+                            }
+                        } else if (lane == 0) {
+                            atomicOr(a.overflow, 1u);
+                        }
+                    }
+                    cnt++;
+                    start = (uint32_t)k + 1;
+                }
+                if (lane == 0) {
+                    s_done[n & 1] = start >= r1;
+                    if (start >= r1) {
+                        if constexpr (SPEC) {
+                            a.spec_cnt[item] = cnt < a.spec_cap ? cnt : a.spec_cap;
+                            a.spec_next[item] = start;
+                            if (cnt > a.spec_cap) atomicOr(a.overflow, 2u);  // engine bug guard
+                        } else {
+                            a.counts[b] = cnt < a.cap ? cnt : a.cap;
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // window n+1 staged, walk of window n finished
+            if (s_done[n & 1]) break;
+        }
+    }
+    if constexpr (!SPEC) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < a.nbins; i += 256)
+            if (lhist[i]) atomicAdd(&a.hist[i], lhist[i]);
+    }
+}
+
+// Speculative walk, one wave per (buffer, section): a chunk starts at the section start; record
+// chunk starts until the next start reaches the section end.
+__global__ __launch_bounds__(256) void cdc_resolve_spec_kernel(ResolveArgs a) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nitems = a.nbuf * a.nsec;
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < nitems; item += nw) {
+        const uint32_t b = item / a.nsec;
+        const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
+        const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
+        const uint32_t r0 = (item - b * a.nsec) * a.sec_len;
+        if (r0 >= len) {
+            if (lane == 0) {
+                a.spec_cnt[item] = 0;
+                a.spec_next[item] = len;
+            }
+            continue;
+        }
+        const uint32_t r1 = min(r0 + a.sec_len, len);
+        const uint64_t word0 = off >> 5;
+        uint32_t start = r0, cnt = 0;
+        uint32_t* sp = a.spec_starts + (uint64_t)item * a.spec_cap;
+        while (start < r1) {
+            const uint32_t lo = start + a.first_off;
+            const uint32_t forced = start + a.max_len - 1;
+            const uint32_t hi = forced < len - 1 ? forced : len - 1;
+            int64_t k = -1;
+            if (lo <= hi) k = find_first_wide(a.bitmap, word0, lo, hi, lane);
+            if (k < 0) k = (int64_t)hi;
+            if (lane == 0 && cnt < a.spec_cap) sp[cnt] = start;
+            cnt++;
+            start = (uint32_t)k + 1;
+        }
+        if (lane == 0) {
+            a.spec_cnt[item] = cnt < a.spec_cap ? cnt : a.spec_cap;
+            a.spec_next[item] = start;
+            if (cnt > a.spec_cap) atomicOr(a.overflow, 2u);  // capacity is sized so this cannot happen
+        }
+    }
+}
+
+// Stitch: one wave per buffer follows the true cut chain.  Where it lands on a section's
+// speculative chunk start the two chains coincide from there on (same greedy rule, same bits),
+// so the rest of that section's list is copied wave-parallel; otherwise it takes one true step
+// (bitmap search) and tries again.  On random data the chains meet within a chunk or two.
+__global__ __launch_bounds__(256) void cdc_resolve_stitch_kernel(ResolveArgs a) {
+    __shared__ uint32_t lhist[kMaxBins];
+    for (uint32_t i = threadIdx.x; i < a.nbins; i += 256) lhist[i] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < a.nbuf; b += nw) {
+        const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
+        const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
+        const uint64_t word0 = off >> 5;
+        uint32_t p = 0, cnt = 0;
+        while (p < len) {
+            const uint32_t item = b * a.nsec + p / a.sec_len;
+            const uint32_t cm = a.spec_cnt[item];
+            const uint32_t* sp = a.spec_starts + (uint64_t)item * a.spec_cap;
+            int32_t found = -1;
+            for (uint32_t j0 = 0; j0 < cm; j0 += 64) {
+                const uint32_t e = j0 + lane < cm ? sp[j0 + lane] : 0xFFFFFFFFu;
+                const uint64_t hit = __ballot(e == p);
+                if (hit) {
+                    found = (int32_t)(j0 + __builtin_ctzll(hit));
+                    break;
+                }
+                if (__ballot(e > p)) break;  // sorted: p is not a speculative start
+            }
+            if (found >= 0) {
+                const uint32_t nxt = a.spec_next[item];
+                for (uint32_t j0 = (uint32_t)found; j0 < cm; j0 += 64) {
+                    const uint32_t j = j0 + lane;
+                    if (j < cm) {
+                        const uint32_t st = sp[j];
+                        const uint32_t en = j + 1 < cm ? sp[j + 1] : nxt;
+                        const uint32_t clen = en - st;
+                        const uint32_t c = cnt + (j - (uint32_t)found);
+                        if (c < a.cap) {
+                            const uint64_t slot = (uint64_t)b * a.cap + c;
+                            a.starts[slot] = st;
+                            a.clens[slot] = clen;
+                            uint32_t bin = sha_blocks(clen) >> a.bin_shift;
+                            bin = bin < a.nbins ? bin : a.nbins - 1;
+                            atomicAdd(&lhist[bin], 1u);
+                        } else {
+                            atomicOr(a.overflow, 1u);
+                        }
+                    }
+                }
+                cnt += cm - (uint32_t)found;
+                p = nxt;
+            } else {
+                const uint32_t lo = p + a.first_off;
+                const uint32_t forced = p + a.max_len - 1;
+                const uint32_t hi = forced < len - 1 ? forced : len - 1;
+                int64_t k = -1;
+                if (lo <= hi) k = find_first_wide(a.bitmap, word0, lo, hi, lane);
+                if (k < 0) k = (int64_t)hi;
+                const uint32_t clen = (uint32_t)k + 1 - p;
+                if (cnt < a.cap) {
+                    if (lane == 0) {
+                        const uint64_t slot = (uint64_t)b * a.cap + cnt;
+                        a.starts[slot] = p;
+                        a.clens[slot] = clen;
+                        uint32_t bin = sha_blocks(clen) >> a.bin_shift;
+                        bin = bin < a.nbins ? bin : a.nbins - 1;
+                        atomicAdd(&lhist[bin], 1u);
+                    }
+                } else if (lane == 0) {
+                    atomicOr(a.overflow, 1u);
+                }
+                cnt++;
+                p = (uint32_t)k + 1;
+            }
+        }
+        if (lane == 0) a.counts[b] = cnt < a.cap ? cnt : a.cap;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.nbins; i += 256)
+        if (lhist[i]) atomicAdd(&a.hist[i], lhist[i]);
+}
+
+uint32_t resolve_section_len(uint64_t len, uint32_t max_len) {
+    // sections of 1 Mi positions for buffers of 4 MiB and more (40 MiB backup buffers: 40 sections)
+    if (len < (4ull << 20) || len >= (1ull << 31) || (uint64_t)max_len + 64 >= 32ull * kResStride) return 0;
+    return 1u << 20;
+}
+
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
+    const uint64_t len = a.uniform_len ? a.uniform_len : a.max_buf_len;
+    if (a.sec_len && a.spec_starts && a.nbuf) {
+        // very long buffers: speculative walk per section (one workgroup each), then stitch
+        const uint64_t items = (uint64_t)a.nbuf * a.nsec;
+        hipLaunchKernelGGL(cdc_resolve_spec_kernel, dim3((uint32_t)std::min<uint64_t>((items + 3) / 4, 1u << 20)),
+                           dim3(256), 0, s, a);
+        hipLaunchKernelGGL(cdc_resolve_stitch_kernel, dim3((a.nbuf + 3) / 4), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    if (len > 32ull * kResWin && a.max_len + 64ull < 32ull * kResStride && len < (1ull << 31)) {
+        // long buffers: LDS-staged walk, one workgroup per buffer
+        hipLaunchKernelGGL(cdc_resolve_lds_kernel<false>, dim3(a.nbuf ? a.nbuf : 1), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     uint32_t blocks = (a.nbuf + 3) / 4;
     // a few buffers per wave so the per-block histogram flush is amortised
     blocks = (blocks + 3) / 4;

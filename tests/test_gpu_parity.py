@@ -284,6 +284,51 @@ def test_backup_volume_profile_40mib_buffer():
     e.destroy()
 
 
+@pytest.mark.parametrize("prm", [P(max_len=131072), P(), P(max_len=131072, pred_mask=0xFFFFFF)],
+                         ids=["backup", "default", "forced-cuts"])
+def test_long_ragged_buffers_lds_walk(prm):
+    """Buffers longer than one 256 Ki-position LDS window take the LDS-staged cut walk; lengths
+    are unaligned so windows restage mid-buffer and the tail chunk ends inside a window."""
+    lens = np.array([5 * 2**20 + 13, 300 * 1024 - 7, 2**20, 33, 2 * 2**20 + 1000], dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    base = O.synth(SYNTH_SEED, 41, 0, int(offs[-1] + lens[-1]))
+    counts, st, ln, dg = engine_for(prm).chunk_batch(base, offs, lens)
+    for b in range(len(lens)):
+        buf = base[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+        exp = O.chunk(buf, O.Params(**prm))
+        c = counts[b]
+        assert_same((st[b, :c], ln[b, :c], dg[b, :c]), exp, b)
+
+
+def test_sectioned_walk_chains_that_never_meet():
+    """All-zero data cuts at every min_len+1 bytes; with min_len+1 not dividing the 1 Mi-position
+    section length the speculative chains never meet the true one, so the stitch pass walks every
+    cut itself (slow path) and must still be exact."""
+    prm = P(min_len=2999, max_len=131072)
+    lens = np.array([6 * 2**20 + 5, 4 * 2**20], dtype=np.uint32)
+    offs = np.array([0, int(lens[0]) + 59], dtype=np.uint64)
+    base = np.zeros(int(offs[-1] + lens[-1]), dtype=np.uint8)
+    base[int(offs[1]) + 1_500_000:int(offs[1]) + 1_600_000] = 7  # a patch of other bytes
+    counts, st, ln, dg = engine_for(prm).chunk_batch(base, offs, lens)
+    for b in range(len(lens)):
+        buf = base[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+        c = counts[b]
+        assert_same((st[b, :c], ln[b, :c], dg[b, :c]), O.chunk(buf, O.Params(**prm)), b)
+
+
+def test_device_backup_uniform_40mib_batch():
+    """configs[4] shape on the device path: uniform 40 MiB buffers (LDS-staged cut walk)."""
+    prm = P(max_len=131072)
+    e = engine_for(prm)
+    nbuf = 3
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=40960 * 1024, records=False)
+    batch.fill_streams(first_stream=700, bufs_per_stream=1)
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 1, 700, [0, 1, 2])
+
+
 def test_device_error_paths_raise():
     e = engine_for(P())
     batch = DeviceBatch(e, nbuf=2, buf_len=262144, records=False)
