@@ -477,9 +477,10 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
 }
 
 // variant table (id 0 = production default; the others are built only for sweeps).  Production:
-// 32 conflict-free table copies, one segment per lane, one whole 128-byte line per lane per load
-// (measured 1.56 ms / 4 GiB on MI355X vs 2.6 ms with 64-byte loads, DESIGN.md "Scan variants").
-using ScanV0 = ScanCfg<32, 1, false, 4, 0, 128>;
+// 32 conflict-free table copies, one segment per lane, two whole 128-byte lines per lane per
+// iteration (interleaved A/B on MI355X, scripts/ab.py: 1.56 ms / 4 GiB vs 1.78 ms with one line
+// (variant 7) and 2.6 ms with 64-byte loads; DESIGN.md "Scan variants").
+using ScanV0 = ScanCfg<32, 1, false, 4, 0, 256>;
 using ScanV16 = ScanCfg<32, 2, false, 4>;  // round-1 first version: 64-byte loads, 2 chains
 using ScanV17 = ScanCfg<32, 2, true, 4, 0, 128>;
 using ScanV1 = ScanCfg<32, 2, true, 4>;
