@@ -155,6 +155,10 @@ int sdfs_cdc_stream_sync(sdfs_cdc_engine* e);
  * recorded events and returns, per pipeline stage, the average milliseconds over the last
  * min(nruns, runs since set_timing) runs; returns the number of stages written. */
 int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns);
+/* The same for a subset of the stages only (bit i = i-th name sdfs_cdc_kernel_times reports:
+ * prep, cdc_scan, cdc_resolve, cdc_prefix, cdc_scatter, chunk_hash, pipeline); untimed stages
+ * report 0.  Fewer events per run = less event overhead in a timed region. */
+int sdfs_cdc_set_timing_mask(sdfs_cdc_engine* e, int nruns, uint32_t stage_mask);
 int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int n);
 
 /* Synthetic input generator, device side: fills d_out[0..n) with byte

@@ -90,6 +90,7 @@ SIGNATURES = {
     "sdfs_cdc_stream_sync": (ctypes.c_int, [_vp]),
     "sdfs_cdc_set_pipeline": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint64]),
     "sdfs_cdc_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "sdfs_cdc_set_timing_mask": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32]),
     "sdfs_cdc_kernel_times": (ctypes.c_int, [_vp, _P(ctypes.c_char_p), _P(ctypes.c_float), ctypes.c_int]),
     "sdfs_cdc_synth_device": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                              ctypes.c_uint64, _vp]),

@@ -10,8 +10,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sdfs_cdc.h"
@@ -117,6 +121,95 @@ enum { K_PREP = 0, K_SCAN, K_RESOLVE, K_PREFIX, K_SCATTER, K_HASH, K_PIPE };
 constexpr int kMaxParts = 16;
 constexpr int kEvPerRun = 2 * (kMaxParts * 5 + 2);
 
+// One slot of the double-buffered host path (host_batch): pinned staging in and out, the
+// device copy of the packed batch and its output slots.  While the GPU chunks the batch in one
+// slot, the host packs the next batch into the other and unpacks the previous one's results.
+struct HostSlot {
+    uint8_t* pin_in = nullptr;
+    size_t pin_in_n = 0;
+    uint8_t* pin_out = nullptr;
+    size_t pin_out_n = 0;
+    DevBuf<uint8_t> data;
+    DevBuf<uint64_t> offs;
+    DevBuf<uint32_t> lens;
+    DevBuf<uint32_t> counts, starts, clens, total;
+    DevBuf<uint8_t> digests;
+    hipEvent_t h2d = nullptr;   // staging -> device copy done (copy stream)
+    hipEvent_t done = nullptr;  // pipeline + device -> pinned results done (engine stream)
+    bool busy = false;
+    uint32_t b0 = 0, n = 0, dcap = 0;
+};
+
+// Pageable caller buffers -> pinned staging, split over a small persistent thread pool (the
+// host memcpy, not PCIe, bounds the host path when it runs on one thread).
+struct CopyPiece {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+};
+
+class CopyPool {
+  public:
+    explicit CopyPool(int workers) {
+        for (int i = 0; i < workers; i++) th_.emplace_back([this] { loop(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(const std::vector<CopyPiece>& p) {
+        if (th_.empty() || p.size() < 2) {
+            for (const auto& x : p) memcpy(x.dst, x.src, x.n);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> l(m_);
+            job_ = &p;
+            next_.store(0);
+            active_ = th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        drain(p);  // the calling thread copies too
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [&] { return active_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void drain(const std::vector<CopyPiece>& p) {
+        for (size_t i; (i = next_.fetch_add(1)) < p.size();) memcpy(p[i].dst, p[i].src, p[i].n);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::vector<CopyPiece>* job;
+            {
+                std::unique_lock<std::mutex> l(m_);
+                cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                job = job_;
+            }
+            drain(*job);
+            std::lock_guard<std::mutex> l(m_);
+            if (--active_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::vector<CopyPiece>* job_ = nullptr;
+    std::atomic<size_t> next_{0};
+    size_t active_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 }  // namespace
 
 struct sdfs_cdc_engine {
@@ -143,17 +236,18 @@ struct sdfs_cdc_engine {
     DevBuf<uint32_t> rec_base;
     DevBuf<uint32_t> tasks;
     DevBuf<uint32_t> spec_starts, spec_cnt, spec_next;  // sectioned cut walk of very long buffers
-    // host-path device buffers
+    // getHash device buffers and pinned staging
     DevBuf<uint8_t> h_data;
-    DevBuf<uint64_t> h_offs;
-    DevBuf<uint32_t> h_lens;
-    DevBuf<uint32_t> o_counts, o_starts, o_lens, o_total;
+    DevBuf<uint32_t> o_starts;
     DevBuf<uint8_t> o_digests;
-    // pinned host staging
     uint8_t* pin_data = nullptr;
     size_t pin_data_n = 0;
-    uint8_t* pin_out = nullptr;
-    size_t pin_out_n = 0;
+    // batched host path: two slots, H2D on its own stream, packing on copy_threads threads
+    HostSlot hs[2];
+    hipStream_t s_h2d = nullptr;
+    int copy_threads = 8;
+    std::unique_ptr<CopyPool> pool;
+    uint32_t timing_mask = 0xFFFFFFFFu;  // stages timed when timing is on (bit = kKernelNames index)
 
     // per-kernel HIP events for the last `timing_slots` runs (ring); averaged by kernel_times
     struct TimedRun {
@@ -211,7 +305,7 @@ uint32_t slot_cap_for(const sdfs_cdc_params& p, uint64_t len) {
 
 // Records a start event for stage `kid` on stream `st` (timing runs only); returns the pair index.
 int t_begin(sdfs_cdc_engine* e, int kid, hipStream_t st) {
-    if (!e->run) return -1;
+    if (!e->run || !((e->timing_mask >> kid) & 1u)) return -1;
     const int i = (int)e->run->kid.size();
     if (2 * i + 1 >= kEvPerRun) return -1;
     e->run->kid.push_back(kid);
@@ -357,7 +451,7 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
         // one wave = one buffer: the fused scan variant resolves inside the scan kernel
         // (single stream only: the histogram it feeds is cleared on the post stream)
         const bool fused = e->scan_info.fuse && parts == 1 && uniform_len && e->scan_info.chains == 1 &&
-                           (uint64_t)uniform_len == 64ull * e->seg_len;
+                           (uint64_t)uniform_len == 64ull * e->seg_len && e->seg_len < 0xFFFFu;
         sa.fuse_resolve = fused ? 1u : 0u;
         sa.res = ra;
         const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
@@ -442,17 +536,54 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
     return SDFS_CDC_OK;
 }
 
-// Host buffers -> device, pipeline, device -> host.  Caller holds e->mu.
-int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t nbuf,
-               uint32_t* counts, uint32_t* starts, uint32_t* lens_out, uint8_t* digests, uint32_t cap) {
-    if (nbuf == 0) return SDFS_CDC_OK;
-    const uint64_t staging = e->prm.max_batch_bytes ? e->prm.max_batch_bytes : (256ull << 20);
-    uint32_t b0 = 0;
+// Results of the batch in slot `sl` (synchronises on it) -> the caller's arrays.
+int drain_slot(sdfs_cdc_engine* e, HostSlot& sl, uint32_t* counts, uint32_t* starts, uint32_t* lens_out,
+               uint8_t* digests, uint32_t cap) {
+    sl.busy = false;
+    HIP_TRY(hipEventSynchronize(sl.done));
+    const uint32_t n = sl.n, dcap = sl.dcap;
+    const uint64_t nout = (uint64_t)n * dcap;
+    const uint32_t* pc = reinterpret_cast<const uint32_t*>(sl.pin_out);
+    const uint32_t* ps = pc + n;
+    const uint32_t* pl = ps + nout;
+    const uint32_t* povf = pl + nout;
+    const uint8_t* pd = reinterpret_cast<const uint8_t*>(povf + 16);
+    if (*povf) return fail(SDFS_CDC_EHIP, "internal: chunk slot overflow");
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t c = pc[i];
+        if (c > cap) return fail(SDFS_CDC_ECAP, "buffer %u has %u chunks > cap %u", sl.b0 + i, c, cap);
+        counts[sl.b0 + i] = c;
+        const uint64_t so = (uint64_t)i * dcap, dst = (uint64_t)(sl.b0 + i) * cap;
+        memcpy(starts + dst, ps + so, c * 4ull);
+        memcpy(lens_out + dst, pl + so, c * 4ull);
+        if (digests)
+            for (uint32_t k = 0; k < c; k++)
+                memcpy(digests + (dst + k) * e->digest_len, pd + (so + k) * 32, e->digest_len);
+    }
+    return SDFS_CDC_OK;
+}
+
+// Host buffers -> device, pipeline, device -> host, double-buffered: batch i is packed into
+// pinned slot i%2 (copy_threads threads) while the GPU copies in and chunks batch i-1, and the
+// results of batch i-2 are unpacked once its slot is needed again.  H2D runs on its own
+// stream; pipeline and D2H on the engine stream.  Caller holds e->mu.
+int host_batch_impl(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
+                    uint32_t nbuf, uint32_t* counts, uint32_t* starts, uint32_t* lens_out, uint8_t* digests,
+                    uint32_t cap) {
+    const uint64_t staging = e->prm.max_batch_bytes ? e->prm.max_batch_bytes : (64ull << 20);
+    if (!e->pool && e->copy_threads > 1) e->pool.reset(new CopyPool(e->copy_threads - 1));
+    hipStream_t s = e->stream;
+    std::vector<CopyPiece> pieces;
+    uint32_t b0 = 0, k = 0;
     while (b0 < nbuf) {
+        HostSlot& sl = e->hs[k++ & 1];
+        if (sl.busy) {
+            const int rc = drain_slot(e, sl, counts, starts, lens_out, digests, cap);
+            if (rc) return rc;
+        }
         // pack as many buffers as fit (at 64-byte aligned offsets)
-        uint64_t bytes = 0;
+        uint64_t bytes = 0, maxlen = 1;
         uint32_t b1 = b0;
-        uint64_t maxlen = 1;
         while (b1 < nbuf) {
             const uint64_t need = (lens[b1] + 63ull) & ~63ull;
             if (b1 > b0 && bytes + need > staging) break;
@@ -462,69 +593,90 @@ int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, co
         }
         const uint32_t n = b1 - b0;
         const uint32_t dcap = slot_cap_for(e->prm, maxlen);
-        int rc = pinned_ensure(&e->pin_data, &e->pin_data_n, bytes + n * 12ull + 64);
+        int rc = pinned_ensure(&sl.pin_in, &sl.pin_in_n, ((bytes + 63) & ~63ull) + n * 12ull + 64);
         if (rc) return rc;
-        uint64_t* hoffs = reinterpret_cast<uint64_t*>(e->pin_data + ((bytes + 63) & ~63ull));
+        uint64_t* hoffs = reinterpret_cast<uint64_t*>(sl.pin_in + ((bytes + 63) & ~63ull));
         uint32_t* hlens = reinterpret_cast<uint32_t*>(hoffs + n);
+        pieces.clear();
         uint64_t o = 0;
+        constexpr size_t kPiece = 1u << 20;
         for (uint32_t i = 0; i < n; i++) {
-            memcpy(e->pin_data + o, base + offs[b0 + i], lens[b0 + i]);
+            const uint8_t* src = base + offs[b0 + i];
+            for (size_t q = 0; q < lens[b0 + i]; q += kPiece)
+                pieces.push_back({sl.pin_in + o + q, src + q, std::min<size_t>(kPiece, lens[b0 + i] - q)});
             hoffs[i] = o;
             hlens[i] = lens[b0 + i];
             o += (lens[b0 + i] + 63ull) & ~63ull;
         }
-        HIP_TRY(e->h_data.ensure(std::max<uint64_t>(bytes, 64)));
-        HIP_TRY(e->h_offs.ensure(n));
-        HIP_TRY(e->h_lens.ensure(n));
-        HIP_TRY(e->o_counts.ensure(n));
-        HIP_TRY(e->o_starts.ensure((uint64_t)n * dcap));
-        HIP_TRY(e->o_lens.ensure((uint64_t)n * dcap));
-        HIP_TRY(e->o_digests.ensure((uint64_t)n * dcap * 32));
-        HIP_TRY(e->o_total.ensure(1));
-        hipStream_t s = e->stream;
-        HIP_TRY(hipMemcpyAsync(e->h_data.p, e->pin_data, bytes, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(e->h_offs.p, hoffs, n * 8ull, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(e->h_lens.p, hlens, n * 4ull, hipMemcpyHostToDevice, s));
-        sdfs_cdc_dev_out out{};
-        out.counts = e->o_counts.p;
-        out.starts = e->o_starts.p;
-        out.lens = e->o_lens.p;
-        out.digests = e->o_digests.p;
-        out.cap = dcap;
-        out.total = e->o_total.p;
-        rc = run_pipeline(e, e->h_data.p, bytes, e->h_offs.p, e->h_lens.p, n, 0, 0, &out, s, maxlen);
-        if (rc) return rc;
-        // results back through pinned memory
+        if (e->pool && bytes >= (4u << 20))
+            e->pool->run(pieces);
+        else
+            for (const auto& x : pieces) memcpy(x.dst, x.src, x.n);
+        HIP_TRY(sl.data.ensure(std::max<uint64_t>(bytes, 64)));
+        HIP_TRY(sl.offs.ensure(n));
+        HIP_TRY(sl.lens.ensure(n));
+        HIP_TRY(sl.counts.ensure(n));
+        HIP_TRY(sl.starts.ensure((uint64_t)n * dcap));
+        HIP_TRY(sl.clens.ensure((uint64_t)n * dcap));
+        HIP_TRY(sl.digests.ensure((uint64_t)n * dcap * 32));
+        HIP_TRY(sl.total.ensure(1));
         const uint64_t nout = (uint64_t)n * dcap;
-        const size_t out_bytes = n * 4ull + nout * 8 + nout * 32 + 64;
-        rc = pinned_ensure(&e->pin_out, &e->pin_out_n, out_bytes);
+        rc = pinned_ensure(&sl.pin_out, &sl.pin_out_n, n * 4ull + nout * 8 + 64 + nout * 32 + 64);
         if (rc) return rc;
-        uint32_t* pc = reinterpret_cast<uint32_t*>(e->pin_out);
+        HIP_TRY(hipMemcpyAsync(sl.data.p, sl.pin_in, bytes, hipMemcpyHostToDevice, e->s_h2d));
+        HIP_TRY(hipMemcpyAsync(sl.offs.p, hoffs, n * 8ull, hipMemcpyHostToDevice, e->s_h2d));
+        HIP_TRY(hipMemcpyAsync(sl.lens.p, hlens, n * 4ull, hipMemcpyHostToDevice, e->s_h2d));
+        HIP_TRY(hipEventRecord(sl.h2d, e->s_h2d));
+        HIP_TRY(hipStreamWaitEvent(s, sl.h2d, 0));
+        sdfs_cdc_dev_out out{};
+        out.counts = sl.counts.p;
+        out.starts = sl.starts.p;
+        out.lens = sl.clens.p;
+        out.digests = sl.digests.p;
+        out.cap = dcap;
+        out.total = sl.total.p;
+        rc = run_pipeline(e, sl.data.p, bytes, sl.offs.p, sl.lens.p, n, 0, 0, &out, s, maxlen);
+        if (rc) return rc;
+        // results back through pinned memory: counts | starts | lens | overflow flag (64 B) | digests
+        uint32_t* pc = reinterpret_cast<uint32_t*>(sl.pin_out);
         uint32_t* ps = pc + n;
         uint32_t* pl = ps + nout;
-        uint8_t* pd = reinterpret_cast<uint8_t*>(pl + nout);
+        uint32_t* povf = pl + nout;
+        uint8_t* pd = reinterpret_cast<uint8_t*>(povf + 16);
         HIP_TRY(hipMemcpyAsync(pc, out.counts, n * 4ull, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(ps, out.starts, nout * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(pl, out.lens, nout * 4, hipMemcpyDeviceToHost, s));
+        // the run-wide overflow flag, read before the next batch's pipeline clears it
+        HIP_TRY(hipMemcpyAsync(povf, e->small.p + 2 * kMaxBins, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(pd, out.digests, nout * 32, hipMemcpyDeviceToHost, s));
-        uint32_t ovf = 0;
-        HIP_TRY(hipMemcpyAsync(&ovf, e->small.p + 2 * kMaxBins, 4, hipMemcpyDeviceToHost, s));  // run-wide flag
-        HIP_TRY(hipStreamSynchronize(s));
-        if (ovf) return fail(SDFS_CDC_EHIP, "internal: chunk slot overflow");
-        for (uint32_t i = 0; i < n; i++) {
-            const uint32_t c = pc[i];
-            if (c > cap) return fail(SDFS_CDC_ECAP, "buffer %u has %u chunks > cap %u", b0 + i, c, cap);
-            counts[b0 + i] = c;
-            const uint64_t so = (uint64_t)i * dcap, dst = (uint64_t)(b0 + i) * cap;
-            memcpy(starts + dst, ps + so, c * 4ull);
-            memcpy(lens_out + dst, pl + so, c * 4ull);
-            if (digests)
-                for (uint32_t k = 0; k < c; k++)
-                    memcpy(digests + (dst + k) * e->digest_len, pd + (so + k) * 32, e->digest_len);
-        }
+        HIP_TRY(hipEventRecord(sl.done, s));
+        sl.busy = true;
+        sl.b0 = b0;
+        sl.n = n;
+        sl.dcap = dcap;
         b0 = b1;
     }
+    // the older batch first
+    for (int j = 0; j < 2; j++) {
+        HostSlot& sl = e->hs[(k + j) & 1];
+        if (sl.busy) {
+            const int rc = drain_slot(e, sl, counts, starts, lens_out, digests, cap);
+            if (rc) return rc;
+        }
+    }
     return SDFS_CDC_OK;
+}
+
+int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t nbuf,
+               uint32_t* counts, uint32_t* starts, uint32_t* lens_out, uint8_t* digests, uint32_t cap) {
+    if (nbuf == 0) return SDFS_CDC_OK;
+    const int rc = host_batch_impl(e, base, offs, lens, nbuf, counts, starts, lens_out, digests, cap);
+    if (rc) {  // leave no batch in flight behind a failed call
+        (void)hipStreamSynchronize(e->s_h2d);
+        (void)hipStreamSynchronize(e->stream);
+        e->hs[0].busy = e->hs[1].busy = false;
+    }
+    return rc;
 }
 
 }  // namespace
@@ -580,10 +732,16 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
         hipStreamCreateWithFlags(&e->s_scan, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->s_post, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_done, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&e->ev_done, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->hs[0].h2d, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->hs[0].done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->hs[1].h2d, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->hs[1].done, hipEventDisableTiming) != hipSuccess) {
         sdfs_cdc_destroy(e);
         return fail(SDFS_CDC_EHIP, "stream/event creation failed");
     }
+    if (const char* v = getenv("SDFS_COPY_THREADS")) e->copy_threads = std::max(1, std::min(atoi(v), 64));
     for (auto& ev : e->ev_scan)
         if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
             sdfs_cdc_destroy(e);
@@ -628,15 +786,22 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
         e->spec_cnt.release();
         e->spec_next.release();
         e->h_data.release();
-        e->h_offs.release();
-        e->h_lens.release();
-        e->o_counts.release();
         e->o_starts.release();
-        e->o_lens.release();
-        e->o_total.release();
         e->o_digests.release();
         if (e->pin_data) (void)hipHostFree(e->pin_data);
-        if (e->pin_out) (void)hipHostFree(e->pin_out);
+        if (e->s_h2d) (void)hipStreamSynchronize(e->s_h2d);
+        for (auto& sl : e->hs) {
+            if (sl.pin_in) (void)hipHostFree(sl.pin_in);
+            if (sl.pin_out) (void)hipHostFree(sl.pin_out);
+            for (auto* b : {&sl.counts, &sl.starts, &sl.clens, &sl.total}) b->release();
+            sl.data.release();
+            sl.offs.release();
+            sl.lens.release();
+            sl.digests.release();
+            if (sl.h2d) (void)hipEventDestroy(sl.h2d);
+            if (sl.done) (void)hipEventDestroy(sl.done);
+        }
+        e->pool.reset();
         if (e->s_scan) (void)hipStreamSynchronize(e->s_scan);
         if (e->s_post) (void)hipStreamSynchronize(e->s_post);
         for (auto& run : e->ev_runs)
@@ -649,6 +814,7 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
         if (e->stream) (void)hipStreamDestroy(e->stream);
         if (e->s_scan) (void)hipStreamDestroy(e->s_scan);
         if (e->s_post) (void)hipStreamDestroy(e->s_post);
+        if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
     }
     delete e;
     return SDFS_CDC_OK;
@@ -686,10 +852,13 @@ int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64
     return run_pipeline(e, d_data, data_bytes, d_offs, d_lens, nbuf, 0, buffer_id_base, out, s, max_len_hint);
 }
 
-int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns) {
+int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns) { return sdfs_cdc_set_timing_mask(e, nruns, 0xFFFFFFFFu); }
+
+int sdfs_cdc_set_timing_mask(sdfs_cdc_engine* e, int nruns, uint32_t stage_mask) {
     if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
     if (nruns < 0 || nruns > 4096) return fail(SDFS_CDC_EINVAL, "timing slots %d", nruns);
     std::lock_guard<std::mutex> lk(e->mu);
+    e->timing_mask = stage_mask;
     HIP_TRY(hipSetDevice(e->prm.device));
     while ((int)e->ev_runs.size() < nruns) {
         sdfs_cdc_engine::TimedRun r;

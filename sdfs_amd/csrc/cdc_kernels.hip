@@ -308,13 +308,91 @@ __device__ __forceinline__ void resolve_buffer(const ResolveArgs& a, uint32_t b,
     }
 }
 
+// Candidate summary of one scan segment: the first kSumCands candidate offsets (segment-relative,
+// u16) shifted into a 128-bit register quadruple, newest in the low half of s[0]; unused slots
+// hold 0xFFFF.  ncand counts every candidate of the segment (> kSumCands = overflow).
+constexpr uint32_t kSumCands = 8;
+
+__device__ __forceinline__ void sum_push(uint32_t (&s)[4], uint32_t& ncand, uint32_t off) {
+    if (ncand < kSumCands) {
+        s[3] = __builtin_amdgcn_alignbit(s[3], s[2], 16);
+        s[2] = __builtin_amdgcn_alignbit(s[2], s[1], 16);
+        s[1] = __builtin_amdgcn_alignbit(s[1], s[0], 16);
+        s[0] = (s[0] << 16) | off;
+    }
+    ncand++;
+}
+
+// Greedy cut walk of buffer b (one wave; lane l scanned segment l of it, seg_len bytes) from
+// the lanes' candidate summaries: the first candidate in [lo, hi] is the smallest candidate of
+// the first lane whose segment holds one there.  A step whose range touches an overflowed
+// segment searches the bitmap instead (same answer; the bitmap is complete).
+__device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint32_t b, uint32_t lane,
+                                                     const uint32_t (&sm)[4], uint32_t ncand, uint32_t seg_len,
+                                                     uint32_t* lhist) {
+    const uint32_t len = a.uniform_len;
+    const uint64_t word0 = ((uint64_t)b * len) >> 5;
+    const uint32_t my_base = lane * seg_len;
+    uint32_t cand[kSumCands];
+#pragma unroll
+    for (uint32_t k = 0; k < kSumCands; k++) {
+        const uint32_t v = (sm[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        cand[k] = v == 0xFFFFu ? 0xFFFFFFFFu : my_base + v;
+    }
+    const uint64_t ovf = __ballot(ncand > kSumCands);
+    uint32_t start = 0, cnt = 0;
+    while (start < len) {
+        const uint32_t lo = start + a.first_off;
+        const uint32_t forced = start + a.max_len - 1;
+        const uint32_t hi = forced < len - 1 ? forced : len - 1;
+        int64_t k = -1;
+        if (lo <= hi) {
+            const uint32_t slo = lo / seg_len, shi = hi / seg_len;
+            const uint64_t rng = (shi >= 63 ? ~0ull : ((2ull << shi) - 1)) & (~0ull << slo);
+            if (ovf & rng) {
+                k = find_first(a.bitmap, word0, lo, hi, lane);
+            } else {
+                uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+                for (uint32_t j = 0; j < kSumCands; j++) {
+                    const uint32_t c = cand[j];
+                    if (c >= lo && c <= hi && c < best) best = c;
+                }
+                const uint64_t m = __ballot(best != 0xFFFFFFFFu);
+                if (m) k = (int64_t)__builtin_amdgcn_readlane(best, (int)__builtin_ctzll(m));
+            }
+        }
+        if (k < 0) k = (int64_t)hi;  // forced cut at max_len, or the tail chunk
+        const uint32_t clen = (uint32_t)(k + 1 - start);
+        if (cnt < a.cap) {
+            if (lane == 0) {
+                const uint64_t slot = (uint64_t)b * a.cap + cnt;
+                a.starts[slot] = start;
+                a.clens[slot] = clen;
+                uint32_t bin = sha_blocks(clen) >> a.bin_shift;
+                bin = bin < a.nbins ? bin : a.nbins - 1;
+                atomicAdd(&lhist[bin], 1u);
+            }
+        } else if (lane == 0) {
+            atomicOr(a.overflow, 1u);
+        }
+        cnt++;
+        start = (uint32_t)k + 1;
+    }
+    if (lane == 0) a.counts[b] = cnt < a.cap ? cnt : a.cap;
+}
+
 // Scan variants (DESIGN.md "Rabin scan"): C lane-private table copies (32: conflict-free,
 // 128 KiB, one 1024-thread workgroup per CU; 16: 2-way, 64 KiB, two workgroups per CU), NCH
 // independent segments per lane, BLK bytes per lane per iteration (128 = one whole cache line
 // per lane per load, so no line is fetched twice), PF = prefetch the next block.
-template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64, bool FUSE = false>
+// FUSE: 0 = separate resolve kernel; 1 = each wave walks its buffer's bitmap in the epilogue
+// (sweep only, measured slower); 2 = each lane keeps its segment's first kSumCands candidate
+// offsets in registers while it scans, and the wave resolves its buffer from them in the epilogue
+// (no bitmap reads unless a segment overflows: DESIGN.md §4).
+template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64, int FUSE = 0>
 struct ScanCfg {
-    static constexpr bool kFuse = FUSE && NCH == 1;  // resolve each wave's buffer in the epilogue
+    static constexpr int kFuse = NCH == 1 ? FUSE : 0;  // resolve each wave's buffer in the epilogue
     static constexpr int kAbl = ABL;
     static constexpr int kCopies = C;
     static constexpr int kChains = NCH;
@@ -337,7 +415,7 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
         const uint4* src = reinterpret_cast<const uint4*>(a.tab_image);
         uint4* dst = reinterpret_cast<uint4*>(tab);
         for (int i = threadIdx.x; i < CFG::kLds / 16; i += kScanThreads) dst[i] = src[i];
-        if constexpr (CFG::kFuse)
+        if constexpr (CFG::kFuse != 0)
             for (uint32_t i = threadIdx.x; i < kMaxBins; i += kScanThreads) lhist[i] = 0;
     }
     __syncthreads();
@@ -390,6 +468,8 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
         uint32_t lo[NCH], hi[NCH];
         uint32_t prev[NCH][16], cur[NCH][BLKW];
         bool cur_full[NCH];
+        uint32_t sm[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};  // FUSE == 2: candidate summary
+        uint32_t ncand = 0;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             if (nblk[c] != 0 && !first[c]) {
@@ -426,6 +506,18 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
             }
             uint32_t words[NCH][BLK / 32];
             block_words<W, PRED64, 0, BLK / 32, NCH, CFG::kAbl, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+            if constexpr (CFG::kFuse == 2) {
+                // candidates are rare (~1 per 4 KiB): a divergent, seldom-taken append
+#pragma unroll
+                for (int w = 0; w < BLK / 32; w++) {
+                    uint32_t bits = blk < nblk[0] ? words[0][w] : 0u;
+                    while (bits) {
+                        const uint32_t off = blk * BLK + 32 * w + __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        if (start[0] + off < end[0]) sum_push(sm, ncand, off);
+                    }
+                }
+            }
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 if (blk < nblk[c]) {
@@ -456,18 +548,23 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
                 }
             }
         }
-        if constexpr (CFG::kFuse) {
+        if constexpr (CFG::kFuse != 0) {
             if (a.fuse_resolve) {
                 // this wave's 64 segments are buffer seg0 / 64: make the lanes' bitmap stores
                 // visible to the whole wave (same CU, so no L1 staleness), then walk its cuts
                 const uint64_t seg0 = base + (threadIdx.x & ~63u);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                if (seg0 < total) resolve_buffer(a.res, (uint32_t)(seg0 >> 6), lane, lhist);
+                if constexpr (CFG::kFuse == 2) {
+                    if (seg0 < total)
+                        resolve_from_summary(a.res, (uint32_t)(seg0 >> 6), lane, sm, ncand, a.seg_len, lhist);
+                } else {
+                    if (seg0 < total) resolve_buffer(a.res, (uint32_t)(seg0 >> 6), lane, lhist);
+                }
             }
         }
     }
-    if constexpr (CFG::kFuse) {
+    if constexpr (CFG::kFuse != 0) {
         if (a.fuse_resolve) {
             __syncthreads();
             for (uint32_t i = threadIdx.x; i < a.res.nbins; i += kScanThreads)
@@ -480,7 +577,8 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
 // 32 conflict-free table copies, one segment per lane, two whole 128-byte lines per lane per
 // iteration (interleaved A/B on MI355X, scripts/ab.py: 1.56 ms / 4 GiB vs 1.78 ms with one line
 // (variant 7) and 2.6 ms with 64-byte loads; DESIGN.md "Scan variants").
-using ScanV0 = ScanCfg<32, 1, false, 4, 0, 256>;
+using ScanV0 = ScanCfg<32, 1, false, 4, 0, 256, 2>;  // + cut resolution from register summaries
+using ScanV20 = ScanCfg<32, 1, false, 4, 0, 256>;    // production before the fused resolve
 using ScanV16 = ScanCfg<32, 2, false, 4>;  // round-1 first version: 64-byte loads, 2 chains
 using ScanV17 = ScanCfg<32, 2, true, 4, 0, 128>;
 using ScanV1 = ScanCfg<32, 2, true, 4>;
@@ -494,7 +592,7 @@ using ScanV8 = ScanCfg<16, 1, false, 8, 0, 128>;
 using ScanV9 = ScanCfg<32, 1, true, 4, 0, 128>;
 using ScanV10 = ScanCfg<32, 1, false, 4, 0, 256>;
 using ScanV15 = ScanCfg<32, 2, false, 4, 0, 256>;
-using ScanV19 = ScanCfg<32, 1, false, 4, 0, 128, true>;  // V0 + cut resolution in the epilogue
+using ScanV19 = ScanCfg<32, 1, false, 4, 0, 128, 1>;  // 128-B blocks + bitmap-walk resolve in the epilogue
 // ablations of the production configuration (ids 11..25)
 using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;   // no pop read
 using ScanA2 = ScanCfg<32, 1, false, 4, 2, 128>;   // no push read
@@ -505,7 +603,7 @@ using ScanA15 = ScanCfg<32, 1, false, 4, 15, 128>; // only the rolling arithmeti
 
 template <class CFG>
 constexpr ScanVariantInfo info_of() {
-    return {CFG::kCopies, CFG::kChains, CFG::kLds, CFG::kWavesPerSimd / 4, CFG::kBlk, CFG::kFuse ? 1 : 0};
+    return {CFG::kCopies, CFG::kChains, CFG::kLds, CFG::kWavesPerSimd / 4, CFG::kBlk, CFG::kFuse};
 }
 
 ScanVariantInfo scan_variant_info(int v) {
@@ -526,6 +624,7 @@ ScanVariantInfo scan_variant_info(int v) {
     case 16: return info_of<ScanV16>();
     case 17: return info_of<ScanV17>();
     case 19: return info_of<ScanV19>();
+    case 20: return info_of<ScanV20>();
     case 11: return info_of<ScanA1>();
     case 12: return info_of<ScanA2>();
     case 13: return info_of<ScanA3>();
@@ -569,7 +668,7 @@ hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, 
     case id: return window == 48 ? launch_scan_wc<48, T>(a, pred64, grid, s) : hipErrorInvalidValue;
     SWEEP_CASE(1, ScanV1) SWEEP_CASE(2, ScanV2) SWEEP_CASE(3, ScanV3) SWEEP_CASE(4, ScanV4)
     SWEEP_CASE(5, ScanV5) SWEEP_CASE(6, ScanV6) SWEEP_CASE(7, ScanV7) SWEEP_CASE(8, ScanV8)
-    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16) SWEEP_CASE(17, ScanV17) SWEEP_CASE(19, ScanV19) SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3)
+    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16) SWEEP_CASE(17, ScanV17) SWEEP_CASE(19, ScanV19) SWEEP_CASE(20, ScanV20) SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3)
     SWEEP_CASE(14, ScanA4) SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15)
 #undef SWEEP_CASE
 #endif

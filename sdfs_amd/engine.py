@@ -256,6 +256,15 @@ class HipVariableSha256HashEngine:
         """Record HIP events around every kernel of the next runs (ring of `nruns`; 0 = off)."""
         check(self._lib.sdfs_cdc_set_timing(self._h, int(nruns)))
 
+    STAGES = ("prep", "cdc_scan", "cdc_resolve", "cdc_prefix", "cdc_scatter", "chunk_hash", "pipeline")
+
+    def set_timing_stages(self, nruns: int, stages) -> None:
+        """Time only the named stages (fewer events inside a timed region)."""
+        mask = 0
+        for s in stages:
+            mask |= 1 << self.STAGES.index(s)
+        check(self._lib.sdfs_cdc_set_timing_mask(self._h, int(nruns), mask))
+
     def kernel_times(self) -> dict[str, float]:
         names = (ctypes.c_char_p * 8)()
         ms = (ctypes.c_float * 8)()
