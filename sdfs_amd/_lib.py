@@ -15,7 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "libsdfs_cdc.so")
 LIB_PATH = os.environ.get("SDFS_CDC_LIB") or DEFAULT_LIB
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "sdfs_cdc.h")
-HEADER_PATHS = [HEADER_PATH, os.path.join(os.path.dirname(HERE), "include", "sdfs_index.h")]
+HEADER_PATHS = [HEADER_PATH] + [os.path.join(os.path.dirname(HERE), "include", h)
+                               for h in ("sdfs_index.h", "sdfs_lz4.h")]
 
 OK, EINVAL, ECAP, EHIP, ENOMEM, ENODEV = 0, -1, -2, -3, -4, -5
 SHA256, SHA256_160, MD5 = 0, 1, 2
@@ -101,6 +102,17 @@ SIGNATURES = {
                                                   _vp, _vp]),
     "sdfs_cdc_index_get": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
     "sdfs_cdc_index_size": (ctypes.c_int, [_vp, _u64p, _u64p]),
+    # include/sdfs_lz4.h
+    "sdfs_cdc_lz4_bound": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "sdfs_cdc_lz4_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P(_vp)]),
+    "sdfs_cdc_lz4_destroy": (ctypes.c_int, [_vp]),
+    "sdfs_cdc_lz4_compress_device": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp,
+                                                    ctypes.c_int, _vp]),
+    "sdfs_cdc_lz4_plan_records": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_uint32, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
+    "sdfs_cdc_lz4_compress": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _u32p]),
+    "sdfs_cdc_lz4_compress_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp,
+                                                   ctypes.c_int]),
 }
 
 _lib = None

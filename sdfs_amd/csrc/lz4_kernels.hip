@@ -1,0 +1,622 @@
+// lz4_kernels.hip — LZ4 block compression of unique chunks on the MI355X (include/sdfs_lz4.h;
+// SURVEY.md §8(f) row 2).
+//
+// Reference: HashBlobArchive.putChunk (HashBlobArchive.java:1281-1289) stores a new chunk as
+// [int nz = chunk.length, big-endian][CompressionUtils.compressLz4(chunk)]; compressLz4 is
+// lz4-java 1.3.0's native fastCompressor (CompressionUtils.java:52-53,118-120), i.e. the bundled
+// C LZ4 r123 greedy parse.  The bytes emitted here are exactly that parse (oracle/lz4_ref.c
+// restates it; mode V19 = LZ4 1.9.x, pinned there against the image's liblz4).
+//
+// MI355X form: one wave per chunk, its hash table in LDS (2^13 x u16 below 64 KiB + 11 bytes,
+// 2^12 x u32 above: 16 KiB either way).  LZ4's match search probes ip, ip+1, ... with a step that
+// grows by one every 64 misses, so the next 64 probe positions are known in closed form until one
+// of them matches: the wave probes 64 at once (one lane each).  A probe must see the table as the
+// serial loop would — the latest EARLIER probe with the same hash, else the table — so probes
+// of one round that share an entry are found through a 1 KiB LDS scratch (write lane id, read it
+// back) and resolved in lane order; the first lane whose candidate matches is the serial loop's
+// match, and only the probes up to it enter the table.  Match extension (64 x 4 bytes per step),
+// the backward catch-up, literal copies (16 B per lane) and the 255-runs of long lengths are
+// wave-parallel; the per-sequence bookkeeping is wave-uniform scalar work.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/sdfs_lz4.h"
+#include "cdc_internal.h"
+
+namespace sdfs {
+namespace {
+
+constexpr uint32_t kMinMatch = 4, kMfLimit = 12, kLastLiterals = 5, kMlMask = 15, kRunMask = 15;
+constexpr uint32_t kLimit64K = 65536 + kMfLimit - 1;  // below: 16-bit position table
+constexpr uint32_t kMaxDistance = 65535;
+constexpr uint32_t kScrBuckets = 1024;  // same-entry detection among one round's 64 probes
+constexpr int kLz4WgPerCu = 8;          // 17 KiB of LDS per one-wave workgroup
+
+struct Lz4Args {
+    const uint8_t* data;
+    const uint64_t* src_off;
+    const uint32_t* src_len;
+    const uint32_t* d_count;
+    uint64_t n_max;
+    uint8_t* out;
+    const uint64_t* dst_off;
+    uint32_t* dst_len;
+    uint32_t framed;
+};
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+__device__ __forceinline__ uint64_t ld64(const uint8_t* p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+
+// table index of the sequence at p (lz4_ref.c hash_at)
+template <int MODE>
+__device__ __forceinline__ uint32_t lz4_hash(const uint8_t* p, bool u16) {
+    if (u16) return (ld32(p) * 2654435761u) >> 19;
+    if constexpr (MODE == SDFS_CDC_LZ4_V19) return (uint32_t)(((ld64(p) << 24) * 889523592379ull) >> 52);
+    return (ld32(p) * 2654435761u) >> 20;
+}
+
+// Offset of probe i from the search start: steps of 1 for the first 65 probes, then the step
+// grows by one every 64 probes (step_i = (63 + i) >> 6 for i >= 1, step_0 = 1).
+__device__ __forceinline__ uint32_t probe_off(uint32_t i) {
+    if (i == 0) return 0;
+    const uint32_t m = i - 1, q = m >> 6, r = m & 63;
+    return 1 + 32 * q * (q + 1) + r * (q + 1);
+}
+
+__device__ __forceinline__ uint32_t tab_get(const uint32_t* t, uint32_t h, bool u16) {
+    return u16 ? (uint32_t) reinterpret_cast<const uint16_t*>(t)[h] : t[h];
+}
+__device__ __forceinline__ void tab_put(uint32_t* t, uint32_t h, uint32_t v, bool u16) {
+    if (u16)
+        reinterpret_cast<uint16_t*>(t)[h] = (uint16_t)v;
+    else
+        t[h] = v;
+}
+
+// a length field past the token nibble: len/255 bytes of 255 and the remainder
+__device__ __forceinline__ uint32_t put_run(uint8_t* dst, uint32_t op, uint32_t len, uint32_t lane) {
+    const uint32_t nff = len / 255;
+    for (uint32_t k = lane; k < nff; k += 64) dst[op + k] = 255;
+    if (lane == 0) dst[op + nff] = (uint8_t)(len - nff * 255);
+    return op + nff + 1;
+}
+
+// n bytes src -> dst (disjoint), 16 bytes per lane per step, four steps in flight
+__device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
+                                           uint32_t lane) {
+    const uint32_t nv = n >> 4;
+    uint32_t k = lane;
+    for (; k + 192 < nv; k += 256) {
+        uint4 v0, v1, v2, v3;
+        __builtin_memcpy(&v0, src + 16 * k, 16);
+        __builtin_memcpy(&v1, src + 16 * (k + 64), 16);
+        __builtin_memcpy(&v2, src + 16 * (k + 128), 16);
+        __builtin_memcpy(&v3, src + 16 * (k + 192), 16);
+        __builtin_memcpy(dst + 16 * k, &v0, 16);
+        __builtin_memcpy(dst + 16 * (k + 64), &v1, 16);
+        __builtin_memcpy(dst + 16 * (k + 128), &v2, 16);
+        __builtin_memcpy(dst + 16 * (k + 192), &v3, 16);
+    }
+    for (; k < nv; k += 64) {
+        uint4 v;
+        __builtin_memcpy(&v, src + 16 * k, 16);
+        __builtin_memcpy(dst + 16 * k, &v, 16);
+    }
+    for (uint32_t b = (nv << 4) + lane; b < n; b += 64) dst[b] = src[b];
+}
+
+// number of equal bytes src[a0+k] == src[b0+k] with a0+k < lim (LZ4_count), 256 per step
+__device__ __forceinline__ uint32_t match_count(const uint8_t* src, uint32_t a0, uint32_t b0, uint32_t lim,
+                                                uint32_t lane) {
+    if (a0 >= lim) return 0;
+    const uint32_t total = lim - a0;
+    for (uint32_t base = 0; base < total; base += 256) {
+        const uint32_t k = base + 4 * lane;
+        uint32_t d;
+        if (k + 4 <= total) {
+            d = ld32(src + a0 + k) ^ ld32(src + b0 + k);
+        } else if (k < total) {
+            d = 0;
+            for (uint32_t t = 0; t < 4; t++)
+                if (k + t >= total || src[a0 + k + t] != src[b0 + k + t]) d |= 0xFFu << (8 * t);
+        } else {
+            d = 0xFFFFFFFFu;
+        }
+        const uint64_t mm = __ballot(d != 0);
+        if (mm) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+            const uint32_t dl = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)l);
+            return base + 4 * l + ((uint32_t)__builtin_ctz(dl) >> 3);
+        }
+    }
+    return total;
+}
+
+// One chunk, one wave (all lanes run the same scalar control flow).  Returns the block length.
+template <int MODE>
+__device__ uint32_t compress_chunk(const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ dst,
+                                   uint32_t* tab, volatile uint8_t* scr, uint32_t lane) {
+    {
+        uint4* t4 = reinterpret_cast<uint4*>(tab);
+        for (uint32_t i = lane; i < 1024; i += 64) t4[i] = make_uint4(0, 0, 0, 0);
+    }
+    asm volatile("" ::: "memory");  // the cleared table before any 16/32-bit entry access
+    const bool u16 = n < kLimit64K;
+    const uint32_t mflimit = n >= kMfLimit ? n - kMfLimit : 0;
+    const uint32_t search_end = MODE == SDFS_CDC_LZ4_V19 ? mflimit + 1 : mflimit;
+    const uint32_t matchlimit = n >= kLastLiterals ? n - kLastLiterals : 0;
+    uint32_t ip = 0, anchor = 0, op = 0;
+
+    if (n >= kMfLimit + 1) {
+        tab_put(tab, lz4_hash<MODE>(src, u16), 0, u16);
+        ip = 1;
+        for (;;) {
+            // ---- find a match: 64 probes per round
+            uint32_t match = 0;
+            bool found = false;
+            for (uint32_t k0 = 0;; k0 += 64) {
+                const uint32_t vi = ip + probe_off(k0 + lane);
+                const uint32_t vn = ip + probe_off(k0 + lane + 1);
+                const bool act = vn <= search_end;  // the serial loop stops before probing past it
+                uint32_t h = 0, cur = 0, cand = 0;
+                if (act) {
+                    cur = ld32(src + vi);
+                    h = u16 ? (cur * 2654435761u) >> 19 : lz4_hash<MODE>(src + vi, false);
+                    cand = tab_get(tab, h, u16);
+                }
+                // probes of this round that share a table entry (or a scratch bucket)
+                const uint32_t bkt = h & (kScrBuckets - 1);
+                if (act) scr[bkt] = (uint8_t)lane;
+                bool cont = act && scr[bkt] != (uint8_t)lane;
+                if (cont) scr[bkt] = 0xFF;
+                if (act && scr[bkt] == 0xFF) cont = true;
+                const uint64_t C = __ballot(cont);
+                // serial order: a probe sees the latest earlier probe with its hash
+                for (uint64_t m = C; m; m &= m - 1) {
+                    const int j = (int)__builtin_ctzll(m);
+                    const uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)h, j);
+                    const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)vi, j);
+                    if (cont && (uint32_t)j < lane && hj == h) cand = vj;
+                }
+                bool eq = false;
+                if (act && (u16 || cand + kMaxDistance >= vi)) eq = ld32(src + cand) == cur;
+                const uint64_t mact = __ballot(act);
+                const uint64_t meq = __ballot(eq);
+                const uint32_t fe = ~mact ? (uint32_t)__builtin_ctzll(~mact) : 64u;
+                const uint32_t fm = meq ? (uint32_t)__builtin_ctzll(meq) : 64u;
+                if (fe < 64 && fe <= fm) break;  // search ended before a match: last literals
+                // the table after probes 0..lim: each entry keeps its latest probe
+                const uint32_t lim = fm < 64 ? fm : 63;
+                bool sup = false;
+                for (uint64_t m = C; m; m &= m - 1) {
+                    const int j = (int)__builtin_ctzll(m);
+                    if ((uint32_t)j > lim) break;
+                    const uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)h, j);
+                    if (cont && (uint32_t)j > lane && hj == h) sup = true;
+                }
+                if (lane <= lim && act && !sup) tab_put(tab, h, vi, u16);
+                asm volatile("" ::: "memory");
+                if (fm < 64) {
+                    ip = (uint32_t)__builtin_amdgcn_readlane((int)vi, (int)fm);
+                    match = (uint32_t)__builtin_amdgcn_readlane((int)cand, (int)fm);
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+            // ---- catch up: extend the match backwards over equal bytes
+            {
+                const uint32_t B = min(ip - anchor, match);
+                uint32_t back = B;
+                for (uint32_t base = 0; base < B; base += 64) {
+                    const uint32_t l = base + lane;
+                    const bool e = l < B && src[ip - 1 - l] == src[match - 1 - l];
+                    const uint64_t ne = __ballot(!e);
+                    if (ne) {
+                        back = base + (uint32_t)__builtin_ctzll(ne);
+                        break;
+                    }
+                }
+                ip -= back;
+                match -= back;
+            }
+            // ---- literal run
+            uint32_t token = op++;
+            uint32_t tokv;
+            {
+                const uint32_t lit = ip - anchor;
+                if (lit >= kRunMask) {
+                    tokv = kRunMask << 4;
+                    op = put_run(dst, op, lit - kRunMask, lane);
+                } else {
+                    tokv = lit << 4;
+                }
+                copy_bytes(dst + op, src + anchor, lit, lane);
+                op += lit;
+            }
+            // ---- a match, possibly followed at once by another one
+            for (;;) {
+                const uint32_t off = ip - match;
+                if (lane == 0) {
+                    dst[op] = (uint8_t)off;
+                    dst[op + 1] = (uint8_t)(off >> 8);
+                }
+                op += 2;
+                const uint32_t ml = match_count(src, ip + kMinMatch, match + kMinMatch, matchlimit, lane);
+                ip += kMinMatch + ml;
+                if (ml >= kMlMask) {
+                    tokv += kMlMask;
+                    op = put_run(dst, op, ml - kMlMask, lane);
+                } else {
+                    tokv += ml;
+                }
+                if (lane == 0) dst[token] = (uint8_t)tokv;
+                anchor = ip;
+                if (ip > mflimit) break;
+                // fill the table at ip-2, then test an immediate match at ip
+                tab_put(tab, lz4_hash<MODE>(src + ip - 2, u16), ip - 2, u16);
+                const uint32_t h = lz4_hash<MODE>(src + ip, u16);
+                const uint32_t m = tab_get(tab, h, u16);
+                tab_put(tab, h, ip, u16);
+                asm volatile("" ::: "memory");
+                if ((u16 || m + kMaxDistance >= ip) && ld32(src + m) == ld32(src + ip)) {
+                    token = op++;
+                    tokv = 0;
+                    match = m;
+                    continue;
+                }
+                break;
+            }
+            if (ip > mflimit) break;
+            ip++;
+        }
+    }
+    // ---- last literals
+    const uint32_t last = n - anchor;
+    if (last >= kRunMask) {
+        if (lane == 0) dst[op] = (uint8_t)(kRunMask << 4);
+        op = put_run(dst, op + 1, last - kRunMask, lane);
+    } else {
+        if (lane == 0) dst[op] = (uint8_t)(last << 4);
+        op++;
+    }
+    copy_bytes(dst + op, src + anchor, last, lane);
+    return op + last;
+}
+
+// One wave per workgroup; chunk c = blockIdx.x + k * gridDim.x (a static stride balances well:
+// hundreds of chunks per workgroup, and a shared counter would serialise ~10^6 dequeues).
+template <int MODE>
+__global__ __launch_bounds__(64) void lz4_compress_kernel(Lz4Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[4096];
+    __shared__ uint8_t scr[kScrBuckets];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
+    for (uint64_t c = blockIdx.x; c < n_items; c += gridDim.x) {
+        const uint32_t n = a.src_len[c];
+        uint8_t* o = a.out + a.dst_off[c];
+        const uint32_t hdr = a.framed ? 4u : 0u;
+        const uint32_t len = compress_chunk<MODE>(a.data + a.src_off[c], n, o + hdr, tab, scr, lane);
+        if (lane == 0) {
+            if (hdr) {
+                o[0] = (uint8_t)(n >> 24);
+                o[1] = (uint8_t)(n >> 16);
+                o[2] = (uint8_t)(n >> 8);
+                o[3] = (uint8_t)n;
+            }
+            a.dst_len[c] = len + hdr;
+        }
+    }
+}
+
+// ---- plan: record -> chunk extent and output room (block-local scan, block-sum scan, add)
+constexpr int kPlanBlock = 1024;
+
+struct PlanArgs {
+    const uint8_t* records;
+    const uint32_t* sel;
+    const uint32_t* d_count;
+    uint64_t n_max;
+    uint64_t id_base;
+    uint32_t uniform_len;
+    uint32_t framed;
+    const uint64_t* buf_offs;
+    uint64_t* src_off;
+    uint32_t* src_len;
+    uint64_t* dst_off;
+    uint64_t* bsum;
+    uint64_t* total;
+};
+
+__device__ __forceinline__ uint64_t block_exclusive_scan64(uint64_t v, uint64_t* lds, uint64_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) lds[wv] = x;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint64_t w = threadIdx.x < kPlanBlock / 64 ? lds[threadIdx.x] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(w, o);
+            if (lane >= (uint32_t)o) w += y;
+        }
+        if (threadIdx.x < kPlanBlock / 64) lds[16 + threadIdx.x] = w;
+    }
+    __syncthreads();
+    total = lds[16 + kPlanBlock / 64 - 1];
+    const uint64_t before = wv ? lds[16 + wv - 1] : 0;
+    const uint64_t res = before + x - v;
+    __syncthreads();
+    return res;
+}
+
+__device__ __forceinline__ uint64_t plan_count(const PlanArgs& a) {
+    return a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
+}
+
+__global__ __launch_bounds__(kPlanBlock) void lz4_plan_local_kernel(PlanArgs a) {
+    __shared__ uint64_t lds[64];
+    const uint64_t n = plan_count(a);
+    const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
+    uint64_t room = 0;
+    if (i < n) {
+        const uint64_t r = a.sel ? a.sel[i] : i;
+        const uint8_t* rec = a.records + r * kRecordBytes;
+        uint64_t bid;
+        uint32_t st, ln;
+        __builtin_memcpy(&bid, rec + 32, 8);
+        __builtin_memcpy(&st, rec + 40, 4);
+        __builtin_memcpy(&ln, rec + 44, 4);
+        const uint64_t b = bid - a.id_base;
+        a.src_off[i] = (a.buf_offs ? a.buf_offs[b] : b * a.uniform_len) + st;
+        a.src_len[i] = ln;
+        room = (uint64_t)ln + ln / 255 + 16 + (a.framed ? 4 : 0);
+    }
+    uint64_t total;
+    const uint64_t ex = block_exclusive_scan64(room, lds, total);
+    if (i < n) a.dst_off[i] = ex;
+    if (threadIdx.x == 0) a.bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kPlanBlock) void lz4_plan_scan_kernel(uint64_t* bsum, uint32_t nblocks,
+                                                                   uint64_t* total_out) {
+    __shared__ uint64_t lds[64];
+    uint64_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += kPlanBlock) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint64_t v = i < nblocks ? bsum[i] : 0;
+        uint64_t total;
+        const uint64_t ex = block_exclusive_scan64(v, lds, total);
+        if (i < nblocks) bsum[i] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0 && total_out) *total_out = carry;
+}
+
+__global__ __launch_bounds__(kPlanBlock) void lz4_plan_add_kernel(PlanArgs a) {
+    const uint64_t n = plan_count(a);
+    const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
+    if (i < n) a.dst_off[i] += a.bsum[blockIdx.x];
+}
+
+template <typename T>
+struct ZBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(want, 1) * sizeof(T));
+        if (e == hipSuccess) n = std::max<size_t>(want, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+}  // namespace sdfs
+
+using namespace sdfs;
+
+struct sdfs_cdc_lz4 {
+    int device = 0;
+    int mode = SDFS_CDC_LZ4_R123;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    ZBuf<uint64_t> bsum;
+    // host-path scratch
+    ZBuf<uint8_t> h_in, h_out;
+    ZBuf<uint64_t> h_soff, h_doff;
+    ZBuf<uint32_t> h_slen, h_dlen;
+    std::mutex mu;
+};
+
+#define LZ_TRY(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t _e = (expr);                                                                       \
+        if (_e != hipSuccess)                                                                         \
+            return fail_status(SDFS_CDC_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                               __FILE__, __LINE__);                                                   \
+    } while (0)
+
+namespace {
+
+int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
+    if (a.n_max == 0) return SDFS_CDC_OK;
+    const uint64_t grid = std::min<uint64_t>(a.n_max, (uint64_t)z->num_cus * kLz4WgPerCu);
+    if (z->mode == SDFS_CDC_LZ4_V19)
+        hipLaunchKernelGGL(lz4_compress_kernel<SDFS_CDC_LZ4_V19>, dim3((uint32_t)grid), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(lz4_compress_kernel<SDFS_CDC_LZ4_R123>, dim3((uint32_t)grid), dim3(64), 0, s, a);
+    LZ_TRY(hipGetLastError());
+    return SDFS_CDC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t sdfs_cdc_lz4_bound(uint64_t n) { return n + n / 255 + 16; }
+
+int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
+    if (!out) return fail_status(SDFS_CDC_EINVAL, "null output");
+    *out = nullptr;
+    if (mode != SDFS_CDC_LZ4_R123 && mode != SDFS_CDC_LZ4_V19)
+        return fail_status(SDFS_CDC_EINVAL, "bad lz4 mode %d", mode);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail_status(SDFS_CDC_ENODEV, "no HIP device %d", device);
+    LZ_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    LZ_TRY(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail_status(SDFS_CDC_ENODEV, "device %d is %s, this build targets gfx950", device, prop.gcnArchName);
+    auto* z = new sdfs_cdc_lz4();
+    z->device = device;
+    z->mode = mode;
+    z->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete z;
+        return fail_status(SDFS_CDC_EHIP, "stream creation failed");
+    }
+    *out = z;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_lz4_destroy(sdfs_cdc_lz4* z) {
+    if (!z) return SDFS_CDC_OK;
+    {
+        std::lock_guard<std::mutex> lk(z->mu);
+        (void)hipSetDevice(z->device);
+        if (z->stream) (void)hipStreamSynchronize(z->stream);
+        z->bsum.release();
+        z->h_in.release();
+        z->h_out.release();
+        z->h_soff.release();
+        z->h_doff.release();
+        z->h_slen.release();
+        z->h_dlen.release();
+        if (z->stream) (void)hipStreamDestroy(z->stream);
+    }
+    delete z;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_lz4_compress_device(sdfs_cdc_lz4* z, const uint8_t* d_data, const uint64_t* d_src_off,
+                                 const uint32_t* d_src_len, const uint32_t* d_count, uint64_t n_max,
+                                 uint8_t* d_out, const uint64_t* d_dst_off, uint32_t* d_dst_len, int framed,
+                                 void* stream) {
+    if (!z) return fail_status(SDFS_CDC_EINVAL, "null compressor");
+    if (n_max && (!d_data || !d_src_off || !d_src_len || !d_out || !d_dst_off || !d_dst_len))
+        return fail_status(SDFS_CDC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(z->mu);
+    LZ_TRY(hipSetDevice(z->device));
+    Lz4Args a{d_data, d_src_off, d_src_len, d_count, n_max, d_out, d_dst_off, d_dst_len, framed ? 1u : 0u};
+    return launch_compress(z, a, reinterpret_cast<hipStream_t>(stream));
+}
+
+int sdfs_cdc_lz4_plan_records(sdfs_cdc_lz4* z, const uint8_t* d_records, const uint32_t* d_sel,
+                              const uint32_t* d_count, uint64_t n_max, uint64_t buffer_id_base,
+                              uint32_t uniform_len, const uint64_t* d_buf_offs, int framed, uint64_t* d_src_off,
+                              uint32_t* d_src_len, uint64_t* d_dst_off, uint64_t* d_total_bytes, void* stream) {
+    if (!z) return fail_status(SDFS_CDC_EINVAL, "null compressor");
+    if (!d_total_bytes) return fail_status(SDFS_CDC_EINVAL, "null total");
+    if (n_max && (!d_records || !d_src_off || !d_src_len || !d_dst_off))
+        return fail_status(SDFS_CDC_EINVAL, "null argument");
+    if (!d_buf_offs && !uniform_len) return fail_status(SDFS_CDC_EINVAL, "buffer offsets or uniform_len required");
+    std::lock_guard<std::mutex> lk(z->mu);
+    LZ_TRY(hipSetDevice(z->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (n_max == 0) {
+        LZ_TRY(hipMemsetAsync(d_total_bytes, 0, 8, s));
+        return SDFS_CDC_OK;
+    }
+    const uint32_t nblocks = (uint32_t)((n_max + kPlanBlock - 1) / kPlanBlock);
+    LZ_TRY(z->bsum.ensure(nblocks));
+    PlanArgs a{d_records, d_sel,     d_count,   n_max,     buffer_id_base, uniform_len,  framed ? 1u : 0u,
+               d_buf_offs, d_src_off, d_src_len, d_dst_off, z->bsum.p,      d_total_bytes};
+    hipLaunchKernelGGL(lz4_plan_local_kernel, dim3(nblocks), dim3(kPlanBlock), 0, s, a);
+    hipLaunchKernelGGL(lz4_plan_scan_kernel, dim3(1), dim3(kPlanBlock), 0, s, z->bsum.p, nblocks, d_total_bytes);
+    hipLaunchKernelGGL(lz4_plan_add_kernel, dim3(nblocks), dim3(kPlanBlock), 0, s, a);
+    LZ_TRY(hipGetLastError());
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_lz4_compress_batch(sdfs_cdc_lz4* z, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
+                                uint32_t n, uint8_t* out, const uint64_t* out_offs, uint32_t* out_lens, int framed) {
+    if (!z) return fail_status(SDFS_CDC_EINVAL, "null compressor");
+    if (n == 0) return SDFS_CDC_OK;
+    if (!base || !offs || !lens || !out || !out_offs || !out_lens)
+        return fail_status(SDFS_CDC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(z->mu);
+    LZ_TRY(hipSetDevice(z->device));
+    // pack the chunks (16-byte aligned) and lay the outputs out back to back
+    std::vector<uint64_t> soff(n), doff(n);
+    uint64_t in_bytes = 0, out_bytes = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (lens[i] >= (1u << 31)) return fail_status(SDFS_CDC_EINVAL, "chunk %u longer than 2 GiB", i);
+        soff[i] = in_bytes;
+        in_bytes += (lens[i] + 15ull) & ~15ull;
+        doff[i] = out_bytes;
+        out_bytes += ((sdfs_cdc_lz4_bound(lens[i]) + (framed ? 4 : 0)) + 15ull) & ~15ull;
+    }
+    std::vector<uint8_t> packed(in_bytes);
+    for (uint32_t i = 0; i < n; i++) memcpy(packed.data() + soff[i], base + offs[i], lens[i]);
+    LZ_TRY(z->h_in.ensure(in_bytes + 16));
+    LZ_TRY(z->h_out.ensure(out_bytes + 16));
+    LZ_TRY(z->h_soff.ensure(n));
+    LZ_TRY(z->h_doff.ensure(n));
+    LZ_TRY(z->h_slen.ensure(n));
+    LZ_TRY(z->h_dlen.ensure(n));
+    hipStream_t s = z->stream;
+    LZ_TRY(hipMemcpyAsync(z->h_in.p, packed.data(), in_bytes, hipMemcpyHostToDevice, s));
+    LZ_TRY(hipMemcpyAsync(z->h_soff.p, soff.data(), n * 8ull, hipMemcpyHostToDevice, s));
+    LZ_TRY(hipMemcpyAsync(z->h_doff.p, doff.data(), n * 8ull, hipMemcpyHostToDevice, s));
+    LZ_TRY(hipMemcpyAsync(z->h_slen.p, lens, n * 4ull, hipMemcpyHostToDevice, s));
+    Lz4Args a{z->h_in.p, z->h_soff.p, z->h_slen.p, nullptr, n, z->h_out.p, z->h_doff.p, z->h_dlen.p,
+              framed ? 1u : 0u};
+    const int rc = launch_compress(z, a, s);
+    if (rc) return rc;
+    std::vector<uint8_t> packed_out(out_bytes);
+    LZ_TRY(hipMemcpyAsync(packed_out.data(), z->h_out.p, out_bytes, hipMemcpyDeviceToHost, s));
+    LZ_TRY(hipMemcpyAsync(out_lens, z->h_dlen.p, n * 4ull, hipMemcpyDeviceToHost, s));
+    LZ_TRY(hipStreamSynchronize(s));
+    for (uint32_t i = 0; i < n; i++) memcpy(out + out_offs[i], packed_out.data() + doff[i], out_lens[i]);
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_lz4_compress(sdfs_cdc_lz4* z, const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
+                          uint32_t* out_len) {
+    if (!z || !out_len || (n && !src) || !dst) return fail_status(SDFS_CDC_EINVAL, "null argument");
+    if (cap < sdfs_cdc_lz4_bound(n))
+        return fail_status(SDFS_CDC_ECAP, "cap %u < bound %llu", cap, (unsigned long long)sdfs_cdc_lz4_bound(n));
+    const uint64_t off = 0, doff = 0;
+    const uint8_t dummy = 0;
+    return sdfs_cdc_lz4_compress_batch(z, n ? src : &dummy, &off, &n, 1, dst, &doff, out_len, 0);
+}
+
+}  // extern "C"

@@ -1,0 +1,197 @@
+"""LZ4 compression of unique chunks (include/sdfs_lz4.h).
+
+CPU: the oracle restatement (oracle/lz4_ref.c) is pinned byte for byte against the image's
+liblz4 1.9.x in its V19 mode; both modes (R123 = lz4-java 1.3.0's bundled r123, the reference;
+V19) decode back to the input with the oracle's decoder and with liblz4; the committed fixtures
+(tests/golden/lz4.json) are reproduced; the putChunk framing (HashBlobArchive.java:1281-1289) is
+[big-endian length][block]; the library fails loudly without a GPU.
+GPU: the HIP compressor, through the C-ABI, against the oracle — single chunks, host batches of
+mixed kinds and lengths (incl. the 64 KiB + 11 table switch), the golden fixtures, and the
+device path fed by the dedup index's new-chunk list.
+Parity status: V19 pinned (liblz4); R123 differs from V19 only in the two rules lz4_ref.c names
+(where the match search stops; 4- vs 5-byte hash of 32-bit tables): those are unpinned."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import cdc_oracle as C
+from oracle import lz4_oracle as Z
+from sdfs_amd import _lib
+from tests import golden_util as G
+from tests.golden.make_lz4_golden import make_input
+
+LENS = [0, 1, 4, 11, 12, 13, 14, 15, 16, 17, 31, 64, 100, 1000, 4095, 4096, 4097, 8192, 32768, 65535, 65536,
+        65546, 65547, 65548, 100000, 131072]
+
+
+def _gen(kind, n, stream=1):
+    if kind == "rand":
+        return C.synth(1, stream, 0, n).tobytes()
+    if kind == "zeros":
+        return bytes(n)
+    if kind == "text":
+        return Z.text_like(1, stream, n).tobytes()
+    if kind == "mixed":
+        return Z.mixed(1, stream, n).tobytes()
+    if kind == "ramp":
+        return (np.arange(n) % 251).astype(np.uint8).tobytes()
+    raise ValueError(kind)
+
+
+KINDS = ["rand", "zeros", "text", "mixed", "ramp"]
+needs_liblz4 = pytest.mark.skipif(Z.system_lz4() is None, reason="no system liblz4 to pin against")
+
+
+@needs_liblz4
+@pytest.mark.parametrize("kind", KINDS)
+def test_oracle_v19_equals_system_liblz4(kind):
+    for n in LENS:
+        d = _gen(kind, n)
+        assert Z.compress(d, Z.V19) == Z.system_compress(d), (kind, n)
+
+
+@needs_liblz4
+@pytest.mark.parametrize("kind", KINDS)
+def test_both_modes_decode_with_both_decoders(kind):
+    for n in LENS:
+        d = _gen(kind, n, stream=7)
+        for mode in (Z.R123, Z.V19):
+            blk = Z.compress(d, mode)
+            assert len(blk) <= Z.bound(n)
+            assert Z.decompress(blk, n) == d and Z.system_decompress(blk, n) == d, (kind, n, mode)
+
+
+def test_oracle_reproduces_lz4_golden_fixtures():
+    fx = G.load("lz4.json")["fixtures"]
+    assert len(fx) >= 100
+    for f in fx:
+        d = make_input(f["input"])
+        assert hashlib.sha256(d).hexdigest() == f["input_sha256"]
+        for name, mode in Z.MODES.items():
+            blk = Z.compress(d, mode)
+            assert len(blk) == f[name]["len"] and hashlib.sha256(blk).hexdigest() == f[name]["sha256"], (f, name)
+
+
+def test_putchunk_framing_and_known_blocks():
+    # HashBlobArchive.putChunk: bf.putInt(nz = chunk.length) (big-endian) then the block
+    d = b"abcabcabcabcabcabcabcabcabcabcabcabc"
+    fr = Z.compress_framed(d)
+    assert fr[:4] == len(d).to_bytes(4, "big") and fr[4:] == Z.compress(d)
+    # LZ4 block of an empty input is one zero token; of < 13 bytes, literals only
+    assert Z.compress(b"") == b"\x00"
+    assert Z.compress(b"hello") == b"\x50hello"
+
+
+def test_lz4_fails_loudly_without_gpu():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    h = ctypes.c_void_p()
+    assert _lib.load().sdfs_cdc_lz4_create(0, 0, ctypes.byref(h)) == _lib.ENODEV and not h.value
+    assert _lib.load().sdfs_cdc_lz4_create(0, 7, ctypes.byref(h)) == _lib.EINVAL
+    assert _lib.load().sdfs_cdc_lz4_bound(65536) == 65536 + 257 + 16
+    from sdfs_amd.lz4 import HipLz4Compressor
+    with pytest.raises(_lib.SdfsCdcError):
+        HipLz4Compressor()
+
+
+# ------------------------------------------------------------------------------------------
+# GPU
+# ------------------------------------------------------------------------------------------
+_COMP = {}
+
+
+def comp(mode):
+    from sdfs_amd.lz4 import HipLz4Compressor
+    if mode not in _COMP:
+        _COMP[mode] = HipLz4Compressor(mode)
+    return _COMP[mode]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [Z.R123, Z.V19], ids=["r123", "v19"])
+def test_gpu_single_chunks_vs_oracle(mode):
+    c = comp(mode)
+    for kind in KINDS:
+        for n in LENS:
+            d = _gen(kind, n, stream=3)
+            assert c.compress(d) == Z.compress(d, mode), (kind, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [Z.R123, Z.V19], ids=["r123", "v19"])
+def test_gpu_batch_mixed_chunks_vs_oracle(mode):
+    rng = np.random.default_rng(4 + mode)
+    parts, lens = [], []
+    for i in range(300):
+        kind = KINDS[i % len(KINDS)]
+        n = int(rng.choice([0, 1, 13, 4096, 8000, 20000, 32768, 65546, 65547, 131072])) if i % 7 == 0 else \
+            int(rng.integers(4096, 33000))
+        parts.append(_gen(kind, n, stream=100 + i))
+        lens.append(n)
+    offs = np.concatenate([[0], np.cumsum([len(p) + 3 for p in parts[:-1]])]).astype(np.uint64)  # unaligned
+    base = np.zeros(int(offs[-1]) + len(parts[-1]) + 8, np.uint8)
+    for o, p in zip(offs, parts):
+        base[int(o): int(o) + len(p)] = np.frombuffer(p, np.uint8)
+    got = comp(mode).compress_chunks(base, offs, np.array(lens, np.uint32), framed=True)
+    for i, p in enumerate(parts):
+        assert got[i] == Z.compress_framed(p, mode), (i, lens[i])
+
+
+@pytest.mark.gpu
+def test_gpu_golden_fixtures():
+    fx = G.load("lz4.json")["fixtures"]
+    for name, mode in Z.MODES.items():
+        datas = [make_input(f["input"]) for f in fx]
+        offs = np.concatenate([[0], np.cumsum([len(d) for d in datas[:-1]])]).astype(np.uint64)
+        base = np.frombuffer(b"".join(datas) + b"\0" * 8, np.uint8)
+        got = comp(mode).compress_chunks(base, offs, np.array([len(d) for d in datas], np.uint32), framed=False)
+        for f, blk in zip(fx, got):
+            assert len(blk) == f[name]["len"] and hashlib.sha256(blk).hexdigest() == f[name]["sha256"], f["input"]
+
+
+@pytest.mark.gpu
+def test_gpu_device_path_new_chunks_from_the_index():
+    """Write path on the device: getChunks batch (50 % duplicate buffers) -> dedup index ->
+    extents of the NEW chunks -> LZ4 putChunk records; each record equals the oracle's."""
+    torch = pytest.importorskip("torch")
+    from sdfs_amd import HipVariableSha256HashEngine
+    from sdfs_amd.device import DeviceBatch
+    from sdfs_amd.index import HipHashesMap
+    e = HipVariableSha256HashEngine()
+    nbuf, L = 64, 262144
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=L)
+    batch.fill_streams(first_stream=900, bufs_per_stream=16)
+    v = batch.data.view(nbuf, L)
+    v[3, 100000:180000] = 0  # a zero hole: compressible chunks
+    for b in range(32, nbuf):
+        v[b].copy_(v[b - 32])
+    batch.run(buffer_id_base=5000)
+    recs = batch.record_table()
+    ix = HipHashesMap(1 << 16)
+    dup, loc, new, nc = ix.put_records(recs, batch.total, pos_base=0)
+    for mode in (Z.R123, Z.V19):
+        c = comp(mode)
+        src_off, src_len, dst_off, total = c.plan_records(recs, sel=new[: recs.shape[0]], count=nc.view(torch.int32),
+                                                          buffer_id_base=5000, uniform_len=L)
+        out = torch.zeros(int(total.item()) + 16, dtype=torch.uint8, device="cuda")
+        dst_len = torch.zeros(src_len.shape[0], dtype=torch.int32, device="cuda")
+        c.compress_device(batch.data, src_off, src_len, out, dst_off, dst_len, count=nc.view(torch.int32))
+        torch.cuda.synchronize()
+        k = int(nc.item())
+        host = batch.data.cpu().numpy()
+        so, sl, do, dl = (t.cpu().numpy()[:k] for t in (src_off, src_len, dst_off, dst_len))
+        ob = out.cpu().numpy()
+        distinct = {bytes(r[:32]) for r in recs.cpu().numpy()}
+        assert k == len(distinct) <= int(recs.shape[0]) // 2  # buffers 32..63 repeat 0..31
+        for i in range(k):
+            chunk = host[int(so[i]): int(so[i]) + int(sl[i])].tobytes()
+            rec = ob[int(do[i]): int(do[i]) + int(dl[i])].tobytes()
+            assert rec == Z.compress_framed(chunk, mode), i
+    ix.destroy()
+    e.destroy()
