@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""LZ4 of unique chunks on one MI355X: device-resident GiB/s of input.
+
+Workload: NBUF write buffers of 256 KiB (default 4096 = 1 GiB) chunked by the engine with the
+reference parameters; every chunk is treated as new (0 % duplicates) and compressed into its
+putChunk record ([BE length][LZ4 block], HashBlobArchive.java:1281-1289).  Two data sets:
+`random` (the B1 synthetic streams: incompressible, the search skips ahead) and `text` (a
+word-salad corpus, ~2.5x compressible: many short matches).  Reports the kernel's device time
+(HIP events on the launch stream), GiB/s of input, the compression ratio, and the CPU oracle
+(oracle/lz4_ref.c, the same parse) on a sample of the same chunks with THREADS host threads.
+One JSON line per data set and mode."""
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from oracle import cdc_oracle as C  # noqa: E402  (CPU baseline and spot checks only)
+from oracle import lz4_oracle as Z  # noqa: E402
+from sdfs_amd import HipVariableSha256HashEngine  # noqa: E402
+from sdfs_amd.device import DeviceBatch  # noqa: E402
+from sdfs_amd.lz4 import HipLz4Compressor  # noqa: E402
+
+NBUF = int(os.environ.get("NBUF", "4096"))
+REPS = int(os.environ.get("REPS", "5"))
+THREADS = int(os.environ.get("THREADS", "16"))
+CPU_SECS = float(os.environ.get("CPU_SECS", "8"))
+MODES = [m for m in os.environ.get("MODES", "r123,v19").split(",") if m]
+SETS = [s for s in os.environ.get("SETS", "random,text").split(",") if s]
+L = 262144
+
+
+def text_corpus(nbytes: int) -> np.ndarray:
+    """Vectorised word salad (the vocabulary of oracle/lz4_oracle.text_like), 64 MiB tiled."""
+    words = [w + b" " for w in Z._WORDS]
+    vocab = np.frombuffer(b"".join(words), np.uint8)
+    wl = np.array([len(w) for w in words])
+    wo = np.concatenate([[0], np.cumsum(wl)[:-1]])
+    base_n = min(nbytes, 64 << 20)
+    nw = base_n // 3 + 16
+    idx = (C.splitmix64_np(np.arange(nw, dtype=np.uint64) + np.uint64(0x5DF5)) % np.uint64(len(words))).astype(np.int64)
+    lens = wl[idx]
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    total = int(lens.sum())
+    within = np.arange(total) - np.repeat(starts, lens)
+    flat = vocab[np.repeat(wo[idx], lens) + within][:base_n]
+    reps = (nbytes + base_n - 1) // base_n
+    return np.tile(flat, reps)[:nbytes]
+
+
+def main():
+    eng = HipVariableSha256HashEngine()
+    batch = DeviceBatch(eng, nbuf=NBUF, buf_len=L)
+    for ds in SETS:
+        if ds == "random":
+            batch.fill_streams(first_stream=0, bufs_per_stream=256)
+        else:
+            batch.data.copy_(torch.from_numpy(text_corpus(NBUF * L)).to(batch.data.device))
+        batch.run()
+        torch.cuda.synchronize()
+        recs = batch.record_table()
+        n = recs.shape[0]
+        for mname in MODES:
+            mode = Z.MODES[mname]
+            comp = HipLz4Compressor(mode)
+            src_off, src_len, dst_off, total = comp.plan_records(recs, uniform_len=L)
+            out = torch.empty(int(total.item()) + 16, dtype=torch.uint8, device="cuda")
+            dst_len = torch.empty(n, dtype=torch.int32, device="cuda")
+            s = torch.cuda.current_stream()
+            comp.compress_device(batch.data, src_off, src_len, out, dst_off, dst_len)  # warm
+            torch.cuda.synchronize()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(s)
+            for _ in range(REPS):
+                comp.compress_device(batch.data, src_off, src_len, out, dst_off, dst_len)
+            ev[1].record(s)
+            torch.cuda.synchronize()
+            ms = ev[0].elapsed_time(ev[1]) / REPS
+            nbytes = NBUF * L
+            clen = int(dst_len.sum().item())
+            # spot check against the oracle
+            host = batch.data.cpu().numpy()
+            so, sl, do, dl = (t.cpu().numpy() for t in (src_off, src_len, dst_off, dst_len))
+            ob = out.cpu().numpy()
+            rng = np.random.default_rng(1)
+            for i in rng.integers(0, n, 32):
+                chunk = host[int(so[i]): int(so[i]) + int(sl[i])]
+                assert ob[int(do[i]): int(do[i]) + int(dl[i])].tobytes() == Z.compress_framed(chunk, mode), i
+            # CPU oracle on a bounded sample of the same chunks (THREADS threads; ctypes drops the GIL)
+            order = rng.permutation(n)
+            t0 = time.perf_counter()
+            done_bytes = 0
+            k = 0
+            with ThreadPoolExecutor(THREADS) as ex:
+                while time.perf_counter() - t0 < CPU_SECS and k < n:
+                    sel = order[k: k + 512]
+                    k += len(sel)
+                    list(ex.map(lambda i: Z.compress_framed(host[int(so[i]): int(so[i]) + int(sl[i])], mode), sel))
+                    done_bytes += int(sl[sel].sum())
+            cpu_secs = time.perf_counter() - t0
+            print(json.dumps({
+                "bench": "lz4_unique_chunks", "data": ds, "mode": mname, "chunks": int(n),
+                "input_gib": round(nbytes / 2**30, 3), "kernel_ms": round(ms, 3),
+                "gibps": round(nbytes / (ms / 1e3) / 2**30, 1), "ratio": round(nbytes / max(clen, 1), 3),
+                "cpu_baseline": {"gibps": round(done_bytes / cpu_secs / 2**30, 3), "threads": THREADS,
+                                 "sample_chunks": int(k), "kind": "port (oracle/lz4_ref.c)"},
+            }), flush=True)
+            comp.destroy()
+    eng.destroy()
+
+
+if __name__ == "__main__":
+    main()
