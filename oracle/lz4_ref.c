@@ -210,3 +210,51 @@ long lz4_ref_compress_framed(int mode, const uint8_t* src, uint32_t n, uint8_t* 
     const long k = lz4_ref_compress(mode, src, n, dst + 4, cap - 4);
     return k < 0 ? k : k + 4;
 }
+
+/* ---- batch over threads (the timed CPU baseline of scripts/lz4_bench.py) ---- */
+#include <pthread.h>
+
+typedef struct {
+    int mode;
+    const uint8_t* base;
+    const uint64_t* offs;
+    const uint32_t* lens;
+    uint8_t* out;
+    const uint64_t* out_offs;
+    uint32_t* out_lens;
+    uint32_t i0, i1;
+    int failed;
+} lz4_job;
+
+static void* lz4_worker(void* arg) {
+    lz4_job* j = (lz4_job*)arg;
+    for (uint32_t i = j->i0; i < j->i1; i++) {
+        const long k = lz4_ref_compress_framed(j->mode, j->base + j->offs[i], j->lens[i], j->out + j->out_offs[i],
+                                               lz4_ref_bound(j->lens[i]) + 4);
+        if (k < 0) j->failed = 1;
+        j->out_lens[i] = (uint32_t)(k < 0 ? 0 : k);
+    }
+    return NULL;
+}
+
+long lz4_ref_compress_batch(int mode, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t n,
+                            uint8_t* out, const uint64_t* out_offs, uint32_t* out_lens, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    lz4_job jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (lz4_job){mode, base, offs, lens, out, out_offs, out_lens,
+                            (uint32_t)((uint64_t)n * t / nthreads), (uint32_t)((uint64_t)n * (t + 1) / nthreads), 0};
+        pthread_create(&th[t], NULL, lz4_worker, &jobs[t]);
+    }
+    long total = 0;
+    int failed = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        failed |= jobs[t].failed;
+    }
+    if (failed) return -1;
+    for (uint32_t i = 0; i < n; i++) total += out_lens[i];
+    return total;
+}

@@ -20,6 +20,10 @@ long lz4_ref_compress(int mode, const uint8_t* src, uint32_t n, uint8_t* dst, ui
 long lz4_ref_compress_framed(int mode, const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap);
 /* Decode one block (independent check of the format); returns the decoded length or -1. */
 long lz4_ref_decompress(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap);
+/* Framed records of chunks base[offs[i] .. + lens[i]) at out + out_offs[i] (room bound + 4),
+ * on nthreads pthreads; returns the total bytes written or -1. */
+long lz4_ref_compress_batch(int mode, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t n,
+                            uint8_t* out, const uint64_t* out_offs, uint32_t* out_lens, int nthreads);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,6 @@ import json
 import os
 import sys
 import time
-from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -92,18 +91,16 @@ def main():
             for i in rng.integers(0, n, 32):
                 chunk = host[int(so[i]): int(so[i]) + int(sl[i])]
                 assert ob[int(do[i]): int(do[i]) + int(dl[i])].tobytes() == Z.compress_framed(chunk, mode), i
-            # CPU oracle on a bounded sample of the same chunks (THREADS threads; ctypes drops the GIL)
+            # CPU oracle (C, THREADS pthreads) on a bounded sample of the same chunks
             order = rng.permutation(n)
-            t0 = time.perf_counter()
-            done_bytes = 0
-            k = 0
-            with ThreadPoolExecutor(THREADS) as ex:
-                while time.perf_counter() - t0 < CPU_SECS and k < n:
-                    sel = order[k: k + 512]
-                    k += len(sel)
-                    list(ex.map(lambda i: Z.compress_framed(host[int(so[i]): int(so[i]) + int(sl[i])], mode), sel))
-                    done_bytes += int(sl[sel].sum())
-            cpu_secs = time.perf_counter() - t0
+            k = min(n, 2048)
+            while True:
+                sel = np.sort(order[:k])
+                _, cpu_secs = Z.compress_batch(host, so[sel], sl[sel], mode, THREADS)
+                if cpu_secs >= CPU_SECS or k >= n:
+                    break
+                k = min(n, int(k * max(2.0, CPU_SECS / max(cpu_secs, 1e-3))))
+            done_bytes = int(sl[sel].sum())
             print(json.dumps({
                 "bench": "lz4_unique_chunks", "data": ds, "mode": mname, "chunks": int(n),
                 "input_gib": round(nbytes / 2**30, 3), "kernel_ms": round(ms, 3),

@@ -124,6 +124,13 @@ def load():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make` or __graft_entry__.build()")
+        # PyTorch-ROCm ships its own libamdhip64 with the same soname: load it first when it is
+        # installed so this library binds to the runtime torch uses (one HIP runtime per process;
+        # the other order leaves torch with "No HIP GPUs are available").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name, None)
