@@ -16,7 +16,7 @@ DEFAULT_LIB = os.path.join(HERE, "libsdfs_cdc.so")
 LIB_PATH = os.environ.get("SDFS_CDC_LIB") or DEFAULT_LIB
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "sdfs_cdc.h")
 HEADER_PATHS = [HEADER_PATH] + [os.path.join(os.path.dirname(HERE), "include", h)
-                               for h in ("sdfs_index.h", "sdfs_lz4.h")]
+                               for h in ("sdfs_index.h", "sdfs_lz4.h", "sdfs_meta.h")]
 
 OK, EINVAL, ECAP, EHIP, ENOMEM, ENODEV = 0, -1, -2, -3, -4, -5
 SHA256, SHA256_160, MD5 = 0, 1, 2
@@ -113,6 +113,10 @@ SIGNATURES = {
     "sdfs_cdc_lz4_compress": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _u32p]),
     "sdfs_cdc_lz4_compress_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp,
                                                    ctypes.c_int]),
+    # include/sdfs_meta.h
+    "sdfs_cdc_map_slot_bytes": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "sdfs_cdc_map_emit": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, _P(DevOut), ctypes.c_uint32, _vp, _vp, _vp,
+                                         ctypes.c_uint32, _vp, _vp, _vp]),
 }
 
 _lib = None
