@@ -61,6 +61,9 @@ int sdfs_cdc_index_put_records(sdfs_cdc_index* ix, const uint8_t* d_records, uin
 int sdfs_cdc_index_get(sdfs_cdc_index* ix, const uint8_t* d_digests, uint64_t n, uint64_t* d_pos,
                        uint64_t* d_refcount, void* stream);
 
+/* Drop every fingerprint (AbstractHashesMap.clear / a fresh map), enqueued on `stream`. */
+int sdfs_cdc_index_clear(sdfs_cdc_index* ix, void* stream);
+
 /* Fingerprints held (synchronises the index's last stream) and slot capacity.
  * (AbstractHashesMap.getSize / getMaxSize) */
 int sdfs_cdc_index_size(sdfs_cdc_index* ix, uint64_t* used, uint64_t* capacity);

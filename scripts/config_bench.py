@@ -1,0 +1,158 @@
+#!/usr/bin/env python3
+"""The other BASELINE.json configurations on one MI355X, device-resident (bench.py is configs[1]).
+
+CONFIG=dedup  (configs[2]): 8 GiB = 32768 write buffers of 256 KiB, 50 % of them byte copies of
+              an earlier fresh buffer (seeded Bernoulli).  One step = the
+              whole device write path of SparseDedupFile.writeCache for the batch: getChunks
+              (CDC + SHA-256), the dedup-hit index (fresh per step), and the SparseDataChunk
+              map images; LZ4 of the new chunks is timed beside it (on for compressed volumes).
+CONFIG=backup (configs[4], one GPU's slice): BACKUP_VOLUME=true: 102 write buffers of 40 MiB
+              (3.98 GiB), maxLen 128 KiB, tar-like stream (512-byte headers, file bodies of
+              log-uniform length, 20 % of bodies repeating an earlier one); one step = getChunks
+              + the index + LZ4 of the new chunks (backup volumes compress).
+Stage times are HIP events on the launch stream, averaged over STEPS steps.  One JSON line."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from sdfs_amd import HipVariableSha256HashEngine, SdfsConfig  # noqa: E402
+from sdfs_amd.device import DeviceBatch  # noqa: E402
+from sdfs_amd.index import HipHashesMap  # noqa: E402
+from sdfs_amd.lz4 import HipLz4Compressor  # noqa: E402
+from sdfs_amd.meta import emit_map_slots  # noqa: E402
+
+CONFIG = os.environ.get("CONFIG", "dedup")
+STEPS = int(os.environ.get("STEPS", "5"))
+
+
+def fill_dedup(batch, nbuf, L, rng):
+    batch.fill_streams(first_stream=0, bufs_per_stream=256)
+    v = batch.data.view(nbuf, L)
+    fresh = [0]
+    src = np.arange(nbuf)
+    for b in range(1, nbuf):
+        if rng.random() < 0.5:
+            fresh.append(b)
+        else:
+            src[b] = fresh[int(rng.integers(0, len(fresh)))]
+    idx = torch.from_numpy(src).to(batch.data.device)
+    dups = int((src != np.arange(nbuf)).sum())
+    v.copy_(v.index_select(0, idx))  # copies of earlier fresh buffers (fresh ones map to themselves)
+    return dups
+
+
+def fill_backup(batch, total, rng):
+    """512-byte headers + bodies of log-uniform length 1 KiB..64 MiB; 20 % repeat an earlier body."""
+    data = batch.data
+    st = torch.cuda.current_stream().cuda_stream
+    p, k, bodies = 0, 0, []
+    while p < total:
+        h = min(512, total - p)  # header: 512 synthetic bytes
+        batch.engine.synth_device(data.data_ptr() + p, h, 0x7A5, 10**6 + k, 0, stream=st)
+        p += h
+        n = int(min(2 ** rng.uniform(10, 26), total - p))
+        if n <= 0:
+            break
+        if bodies and rng.random() < 0.2:
+            s0, sn = bodies[int(rng.integers(0, len(bodies)))]
+            n = min(n, sn, total - p)
+            data[p:p + n].copy_(data[s0:s0 + n].clone())
+        else:
+            batch.engine.synth_device(data.data_ptr() + p, n, 0x7A5, k, 0, stream=st)
+            bodies.append((p, n))
+        p += n
+        k += 1
+    torch.cuda.synchronize()
+
+
+def main():
+    rng = np.random.default_rng(0x5DF5)
+    if CONFIG == "dedup":
+        cfg = SdfsConfig()
+        nbuf = int(os.environ.get("NBUF", "32768"))
+    else:
+        cfg = SdfsConfig.backup_volume()
+        nbuf = int(os.environ.get("NBUF", "102"))
+    L = cfg.chunk_length
+    eng = HipVariableSha256HashEngine(config=cfg)
+    batch = DeviceBatch(eng, nbuf=nbuf, buf_len=L)
+    dup_bufs = fill_dedup(batch, nbuf, L, rng) if CONFIG == "dedup" else fill_backup(batch, nbuf * L, rng)
+    torch.cuda.synchronize()
+    cap = batch.nbuf * batch.cap
+    ix = HipHashesMap(min(cap, 1 << 29))
+    lz = HipLz4Compressor()
+    s = torch.cuda.current_stream()
+    ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(2)] for k in ("cdc", "index", "meta", "lz4")}
+    acc = {k: 0.0 for k in ev}
+    out = None
+
+    def step(timed):
+        nonlocal out
+        ev["cdc"][0].record(s)
+        batch.run(buffer_id_base=0, stream=s.cuda_stream)
+        ev["cdc"][1].record(s)
+        ev["index"][0].record(s)
+        ix.clear(stream=s.cuda_stream)
+        dup, loc, new, nc = ix.put_records(batch.recs.view(-1, 48), batch.total, pos_base=0, stream=s.cuda_stream)
+        ev["index"][1].record(s)
+        ev["meta"][0].record(s)
+        m, doop, ovf = emit_map_slots(batch, dup, loc, stream=s.cuda_stream)
+        ev["meta"][1].record(s)
+        recs = batch.recs.view(-1, 48)
+        ev["lz4"][0].record(s)
+        so, sl, do, tot = lz.plan_records(recs, sel=new, count=nc.view(torch.int32), uniform_len=L,
+                                          stream=s.cuda_stream)
+        if out is None:
+            room = batch.nbuf * L + batch.nbuf * L // 255 + 20 * cap + (1 << 20)  # >= sum of bound + 4
+            out = torch.empty(room, dtype=torch.uint8, device=batch.data.device)
+        dl = torch.empty(so.shape[0], dtype=torch.int32, device=batch.data.device)
+        lz.compress_device(batch.data, so, sl, out, do, dl, count=nc.view(torch.int32), stream=s.cuda_stream)
+        ev["lz4"][1].record(s)
+        if timed:
+            torch.cuda.synchronize()
+            for k, (a, b) in ev.items():
+                acc[k] += a.elapsed_time(b)
+        return nc, dl, ovf, sl
+
+    step(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(STEPS):
+        nc, dl, ovf, sl = step(True)
+    wall = (time.perf_counter() - t0) / STEPS
+    ms = {k: v / STEPS for k, v in acc.items()}
+    nbytes = nbuf * L
+    total = int(batch.total.item())
+    new = int(nc.item())
+    comp = int(dl[:new].to(torch.int64).sum().item())
+    new_bytes = int(sl[:new].to(torch.int64).sum().item())
+    gib = nbytes / 2**30
+    res = {
+        "bench": f"configs-{CONFIG}", "n_gpus": 1, "steps": STEPS, "input_gib": round(gib, 3),
+        "chunks": total, "mean_chunk_bytes": round(nbytes / total, 1), "new_chunks": new,
+        "dup_chunk_frac": round(1 - new / total, 4),
+        "stage_ms": {k: round(v, 3) for k, v in ms.items()},
+        "gibps": {
+            "cdc_fingerprint": round(gib / (ms["cdc"] / 1e3), 1),
+            "cdc_fingerprint_index": round(gib / ((ms["cdc"] + ms["index"]) / 1e3), 1),
+            "cdc_fingerprint_index_map": round(gib / ((ms["cdc"] + ms["index"] + ms["meta"]) / 1e3), 1),
+            "with_lz4_of_new_chunks": round(gib / (sum(ms.values()) / 1e3), 1),
+        },
+        "lz4_ratio_new_chunks": round(new_bytes / max(comp, 1), 3),
+        "map_overflow": int(ovf.item()),
+        "wall_ms_per_step_incl_event_syncs": round(wall * 1e3, 3),
+    }
+    if CONFIG == "dedup":
+        res["duplicate_buffers"] = dup_bufs
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -427,6 +427,19 @@ int sdfs_cdc_index_get(sdfs_cdc_index* ix, const uint8_t* d_digests, uint64_t n,
     return SDFS_CDC_OK;
 }
 
+int sdfs_cdc_index_clear(sdfs_cdc_index* ix, void* stream) {
+    if (!ix) return fail_status(SDFS_CDC_EINVAL, "null index");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    IX_TRY(hipSetDevice(ix->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    IX_TRY(hipMemsetAsync(ix->table.p, 0, ix->slots * sizeof(IndexSlot), s));
+    IX_TRY(hipMemsetAsync(ix->used.p, 0, sizeof(uint64_t), s));
+    IX_TRY(hipMemsetAsync(ix->overflow.p, 0, sizeof(uint32_t), s));
+    ix->used_ub = 0;
+    ix->last = s;
+    return SDFS_CDC_OK;
+}
+
 int sdfs_cdc_index_size(sdfs_cdc_index* ix, uint64_t* used, uint64_t* capacity) {
     if (!ix) return fail_status(SDFS_CDC_EINVAL, "null index");
     std::lock_guard<std::mutex> lk(ix->mu);

@@ -102,6 +102,13 @@ class HipHashesMap:
         _, ref = self.get_digests(self._digest_tensor([key]))
         return int(ref[0].item())
 
+    def clear(self, stream=None) -> None:
+        """AbstractHashesMap.clear: drop every fingerprint (enqueued on `stream`)."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self._lib.sdfs_cdc_index_clear(self._h, s))
+
     def getSize(self) -> int:
         used, cap = ctypes.c_uint64(), ctypes.c_uint64()
         _lib.check(self._lib.sdfs_cdc_index_size(self._h, ctypes.byref(used), ctypes.byref(cap)))
