@@ -1341,10 +1341,23 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
     }
 }
 
-template <int ALGO, int ABL = 0, int BS = 256, bool PF = false>
+// PRIO: a wave whose chunks are long raises its issue priority.  A chunk's SHA-256 is a serial
+// chain of ~1.4 k VALU instructions per 64-byte block (~2 us per block at full issue rate), so
+// the longest chunk of a batch (up to 2049 blocks with the backup profile's 128 KiB maxLen)
+// sets a floor under the kernel unless its wave is not slowed by the waves sharing its SIMD.
+template <int ALGO, int ABL = 0, int BS = 256, bool PF = false, bool PRIO = false>
 __global__ __launch_bounds__(BS) void chunk_hash_kernel(HashArgs a) {
     const uint32_t i = blockIdx.x * BS + threadIdx.x;
     if (i >= *a.total) return;
+    if constexpr (PRIO) {
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(sha_blocks(a.clens[a.tasks[i]]));
+        if (nb > 1024)
+            __builtin_amdgcn_s_setprio(3);
+        else if (nb > 512)
+            __builtin_amdgcn_s_setprio(2);
+        else if (nb > 256)
+            __builtin_amdgcn_s_setprio(1);
+    }
     hash_task<ALGO, ABL, PF>(a, i);
 }
 
@@ -1384,6 +1397,7 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
             if (!a.wave_ctr || !a.persist_grid) return hipErrorInvalidValue;
             hipLaunchKernelGGL((chunk_hash_persistent_kernel<0, false>), dim3(a.persist_grid), dim3(256), 0, s, a);
             break;
+        case 8: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
