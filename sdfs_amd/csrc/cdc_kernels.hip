@@ -1398,17 +1398,20 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
             hipLaunchKernelGGL((chunk_hash_persistent_kernel<0, false>), dim3(a.persist_grid), dim3(256), 0, s, a);
             break;
         case 8: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 9: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, false>), dim3(blocks), dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
 #endif
     if (variant != 0) return hipErrorInvalidValue;
-    // production: next-block prefetch (measured ~5 % faster on the B1 length mix, 108 VGPRs)
+    // production: next-block prefetch (measured ~5 % faster on the B1 length mix, 108 VGPRs) and
+    // issue priority for waves of long chunks (interleaved A/B: 2.75 vs 2.81 ms per 4 GiB,
+    // profiles/r01/probes/hash_prio_ab.jsonl; sweep variant 9 = without)
     switch (a.algo) {
-    case 0: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true>), dim3(blocks), dim3(256), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((chunk_hash_kernel<1, 0, 256, true>), dim3(blocks), dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((chunk_hash_kernel<2, 0, 256, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((chunk_hash_kernel<1, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((chunk_hash_kernel<2, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

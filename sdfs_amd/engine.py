@@ -79,7 +79,8 @@ class SdfsConfig:
     @classmethod
     def backup_volume(cls, **kw) -> "SdfsConfig":
         """mkfs.sdfs --backup-volume (VolumeConfigWriter.java:298-307)."""
-        return cls(chunk_length=40960 * 1024, max_len=128 * 1024, **kw)
+        kw.setdefault("max_len", 128 * 1024)
+        return cls(chunk_length=40960 * 1024, **kw)
 
     @classmethod
     def from_volume_xml(cls, path: str) -> "SdfsConfig":
