@@ -5,7 +5,7 @@ Runs the B1 workload (64 x 64 MiB, 256 KiB buffers) with the production chunking
 with forced uniform chunk lengths (min_len = L-1, max_len = L: every chunk is exactly L bytes
 except the buffer tail), so the cost of length variance inside and across waves (and of the
 kernel's tail) can be read off against a uniform schedule.  HASH_VARIANTS selects sweep-build
-ablations (1 = no loads, 2 = no compression).  One JSON line per configuration."""
+ablations (1 = no loads, 2 = no compression, 10 = 128-B-aligned loads); SHAPES filters the shapes.  One JSON line per configuration."""
 import json
 import os
 import sys
@@ -23,6 +23,8 @@ nbuf = int(os.environ.get("NBUF", "16384"))
 hvars = [int(v) for v in os.environ.get("HASH_VARIANTS", "0").split(",")]
 shapes = [("production", SdfsConfig())] + [
     (f"uniform{L}", SdfsConfig(min_len=L - 1, max_len=L)) for L in (4096, 8192, 16384, 32768)]
+if os.environ.get("SHAPES"):
+    shapes = [s for s in shapes if s[0] in os.environ["SHAPES"].split(",")]
 data = None
 for name, cfg in shapes:
     for hv in hvars:

@@ -1238,7 +1238,9 @@ __device__ __forceinline__ void load_block64(uint4 (&v)[4], const uint8_t* q) {
 }
 
 // ABL (sweep builds only): 1 = synthesize the message words instead of loading them, 2 = skip the
-// compression (fold the loaded words instead).  Production ABL = 0.
+// compression (fold the loaded words instead), 4 = read from the chunk start rounded down to 128 B
+// (wrong digests; every line is fetched once: the cost of the unaligned-line re-fetch).
+// Production ABL = 0.
 // BS = threads per workgroup; PF = load data block blk+1 while block blk is compressed.
 template <int ALGO, int ABL, bool PF>
 __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
@@ -1250,6 +1252,7 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
     const uint32_t cs = a.starts[slot];
     const uint32_t len = a.clens[slot];
     const uint8_t* p = a.data + boff + cs;
+    if constexpr ((ABL & 4) != 0) p = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(127));
     const uint32_t nfull = len >> 6;           // whole 64-byte data blocks
     const uint32_t nblocks = (len + 8) / 64 + 1;  // + terminator/length block(s)
     const uint64_t bits = (uint64_t)len * 8;
@@ -1399,6 +1402,7 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
             break;
         case 8: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         case 9: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, false>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 10: hipLaunchKernelGGL((chunk_hash_kernel<0, 4, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
