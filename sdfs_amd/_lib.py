@@ -16,7 +16,7 @@ DEFAULT_LIB = os.path.join(HERE, "libsdfs_cdc.so")
 LIB_PATH = os.environ.get("SDFS_CDC_LIB") or DEFAULT_LIB
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "sdfs_cdc.h")
 HEADER_PATHS = [HEADER_PATH] + [os.path.join(os.path.dirname(HERE), "include", h)
-                               for h in ("sdfs_index.h", "sdfs_lz4.h", "sdfs_meta.h")]
+                               for h in ("sdfs_index.h", "sdfs_lz4.h", "sdfs_meta.h", "sdfs_aes.h")]
 
 OK, EINVAL, ECAP, EHIP, ENOMEM, ENODEV = 0, -1, -2, -3, -4, -5
 SHA256, SHA256_160, MD5 = 0, 1, 2
@@ -118,6 +118,19 @@ SIGNATURES = {
     "sdfs_cdc_map_slot_bytes": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "sdfs_cdc_map_emit": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, _P(DevOut), ctypes.c_uint32, _vp, _vp, _vp,
                                          ctypes.c_uint32, _vp, _vp, _vp]),
+    # include/sdfs_aes.h
+    "sdfs_cdc_aes_cbc_bound": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "sdfs_cdc_aes_create": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_uint32, _P(_vp)]),
+    "sdfs_cdc_aes_destroy": (ctypes.c_int, [_vp]),
+    "sdfs_cdc_aes_encrypt_device": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, ctypes.c_int,
+                                                   ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "sdfs_cdc_aes_decrypt_device": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, _vp,
+                                                   _vp, _vp]),
+    "sdfs_cdc_aes_encrypt": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int32, _vp, _vp,
+                                            ctypes.c_uint64, _u64p]),
+    "sdfs_cdc_aes_decrypt": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _u64p]),
+    "sdfs_cdc_aes_encrypt_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_int, ctypes.c_int32,
+                                                  _vp, _vp, _vp, _vp]),
 }
 
 _lib = None
