@@ -109,11 +109,12 @@ void aes_ref_encrypt_block(const uint32_t* rk, int nr, const uint8_t in[16], uin
             for (int c = 0; c < 4; c++) st[r + 4 * c] = t[r + 4 * c];
         if (round != nr) { /* MixColumns */
             for (int c = 0; c < 4; c++) {
-                const uint8_t* a = st + 4 * c;
-                uint8_t b0 = gmul(a[0], 2) ^ gmul(a[1], 3) ^ a[2] ^ a[3];
-                uint8_t b1 = a[0] ^ gmul(a[1], 2) ^ gmul(a[2], 3) ^ a[3];
-                uint8_t b2 = a[0] ^ a[1] ^ gmul(a[2], 2) ^ gmul(a[3], 3);
-                uint8_t b3 = gmul(a[0], 3) ^ a[1] ^ a[2] ^ gmul(a[3], 2);
+                const uint8_t* a = st + 4 * c;  /* {02} = xtime, {03} = xtime ^ identity */
+                const uint8_t x0 = xtime(a[0]), x1 = xtime(a[1]), x2 = xtime(a[2]), x3 = xtime(a[3]);
+                uint8_t b0 = x0 ^ (x1 ^ a[1]) ^ a[2] ^ a[3];
+                uint8_t b1 = a[0] ^ x1 ^ (x2 ^ a[2]) ^ a[3];
+                uint8_t b2 = a[0] ^ a[1] ^ x2 ^ (x3 ^ a[3]);
+                uint8_t b3 = (x0 ^ a[0]) ^ a[1] ^ a[2] ^ x3;
                 st[4 * c] = b0; st[4 * c + 1] = b1; st[4 * c + 2] = b2; st[4 * c + 3] = b3;
             }
         }

@@ -10,6 +10,8 @@ decryption time of the same records, and the CPU oracle (oracle/aes_ref.c, byte-
 no AES-NI) on a sample with THREADS host threads.  One JSON line per variant."""
 import json
 import os
+import shutil
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -31,6 +33,26 @@ VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2").split(",") if v]
 L = 262144
 KEY = A.key_from_passphrase("bench passphrase")
 IV = bytes(range(16))
+
+
+def openssl_speed(threads: int):
+    """AES-256-CBC encrypt throughput of the host's openssl (AES-NI) on 8 KiB records, `threads`
+    processes: the fastest CPU form of the same cipher on this box (GB/s), or None."""
+    exe = shutil.which("openssl")
+    if not exe:
+        return None
+    cmd = [exe, "speed", "-evp", "aes-256-cbc", "-bytes", "8192", "-seconds", "2"]
+    if threads > 1:
+        cmd[2:2] = ["-multi", str(threads)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=60)
+    except (subprocess.TimeoutExpired, OSError):
+        return None
+    for line in r.stdout.splitlines()[::-1]:
+        parts = line.split()
+        if parts and parts[-1].endswith("k") and (parts[0] in ("evp", "AES-256-CBC", "aes-256-cbc")):
+            return round(float(parts[-1][:-1]) * 1e3 / 2**30, 2)
+    return None
 
 
 def main():
@@ -101,6 +123,8 @@ def main():
                 k = min(n, int(k * max(2.0, CPU_SECS / max(cpu_secs, 1e-3))))
             res["cpu_baseline"] = {"gibps": round(int(src_len[sel].sum()) / cpu_secs / 2**30, 4), "threads": THREADS,
                                    "sample_records": int(k), "kind": "port (oracle/aes_ref.c, byte-form FIPS-197)"}
+            res["cpu_openssl_aesni"] = {"gibps_1thread": openssl_speed(1), "gibps": openssl_speed(THREADS),
+                                        "threads": THREADS, "kind": "openssl speed -evp aes-256-cbc, 8 KiB"}
         print(json.dumps(res), flush=True)
         c.destroy()
     eng.destroy()
