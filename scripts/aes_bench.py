@@ -29,7 +29,8 @@ NBUF = int(os.environ.get("NBUF", "4096"))
 REPS = int(os.environ.get("REPS", "5"))
 THREADS = int(os.environ.get("THREADS", "16"))
 CPU_SECS = float(os.environ.get("CPU_SECS", "6"))
-VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2").split(",") if v]
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "7").split(",") if v]
+UNIFORM = int(os.environ.get("UNIFORM", "0"))
 L = 262144
 KEY = A.key_from_passphrase("bench passphrase")
 IV = bytes(range(16))
@@ -67,6 +68,10 @@ def main():
     bid = recs[:, 32:40].copy().view(np.uint64).reshape(n)
     src_off = (bid.astype(np.int64) * L + meta[:, 0].astype(np.int64))
     src_len = meta[:, 1].astype(np.int64)
+    if UNIFORM:  # probe: equal-length records (no long-record critical path)
+        n = NBUF * L // UNIFORM
+        src_off = np.arange(n, dtype=np.int64) * UNIFORM
+        src_len = np.full(n, UNIFORM, np.int64)
     room = (src_len + 4) // 16 * 16 + 16
     dst_off = np.concatenate([[0], np.cumsum(room[:-1])]).astype(np.int64)
     dev = batch.data.device
@@ -107,7 +112,7 @@ def main():
             want = A.cbc_encrypt(KEY, IV, chunk, prefix=b"\xff\xff\xff\xff")
             assert ob[dst_off[i]: dst_off[i] + dl[i]].tobytes() == want, i
         assert (bl == src_len + 4).all()
-        res = {"bench": "aes256_cbc_records", "variant": var, "records": int(n), "input_gib": round(nbytes / 2**30, 3),
+        res = {"bench": "aes256_cbc_records", "variant": var, "uniform_len": UNIFORM or None, "records": int(n), "input_gib": round(nbytes / 2**30, 3),
                "mean_record_bytes": round(nbytes / n + 4, 1), "encrypt_ms": round(enc_ms, 3),
                "encrypt_gibps": round(nbytes / (enc_ms / 1e3) / 2**30, 1), "decrypt_ms": round(dec_ms, 3),
                "decrypt_gibps": round(nbytes / (dec_ms / 1e3) / 2**30, 1)}

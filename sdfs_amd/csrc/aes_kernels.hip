@@ -103,16 +103,35 @@ struct Tab {
     // table word indexed by byte K (0 = least significant) of s
     template <int K>
     __device__ __forceinline__ uint32_t get(uint32_t s) const {
-        if constexpr (COPIES == 64)
+        if constexpr (COPIES == 64 || COPIES == 16)
             return at(__builtin_amdgcn_perm(s, l4, 0x0C0C0000u | ((4u + K) << 8)));
         else
             return at((((s >> (8 * K)) & 255u) << 7) | l4);
+    }
+    // COPIES == 16: the four rotated tables Te0..Te3 side by side, 16 copies each: word (x, t, c)
+    // at byte (x << 8) | (t << 6) | (c << 2), lane l reads copy l & 15 (2-way bank conflicts, no
+    // rotates; one v_perm per lookup).
+    template <int K, int TBL>
+    __device__ __forceinline__ uint32_t get4(uint32_t s) const {
+        return at(__builtin_amdgcn_perm(s, l4 | (TBL << 6), 0x0C0C0000u | ((4u + K) << 8)));
     }
 };
 
 template <int COPIES>
 __device__ __forceinline__ void fill_table(uint32_t* lds, const uint32_t* g, uint32_t nthreads) {
-    for (uint32_t i = threadIdx.x; i < 256u * COPIES; i += nthreads) lds[i] = g[i / COPIES];
+    if constexpr (COPIES == 16) {  // x = i >> 6, table t = (i >> 4) & 3 holds ror(Te0[x], 8t)
+        for (uint32_t i = threadIdx.x; i < 256u * 64u; i += nthreads) {
+            const uint32_t v = g[i >> 6], t = (i >> 4) & 3;
+            lds[i] = t ? __builtin_amdgcn_alignbit(v, v, 8 * t) : v;
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < 256u * COPIES; i += nthreads) lds[i] = g[i / COPIES];
+    }
+}
+
+template <int COPIES>
+constexpr uint32_t tab_words() {
+    return COPIES == 16 ? 256u * 64u : 256u * COPIES;
 }
 
 template <int COPIES>
@@ -327,6 +346,114 @@ __global__ __launch_bounds__(kDecThreads) void aes_cbc_decrypt_kernel(AesDecArgs
     }
 }
 
+// ---- quad form: one record per 4 lanes (lane q of the quad owns state column q)
+// A single lane's CBC chain is a serial ~700-instruction block at 4 cycles per wave64 VALU
+// instruction, so the longest record of a batch (2 k blocks at maxLen 32 KiB) sets the kernel's
+// floor.  Splitting the block's 4 columns over a lane quad cuts that chain ~3.5x: per round a lane
+// fetches its 3 neighbours' columns with DPP quad permutes and does 4 lookups instead of 16.
+template <uint32_t CTRL>
+__device__ __forceinline__ uint32_t quad_mov(uint32_t v) {
+    // mov_dpp (undefined "old"): every lane is written (row/bank masks full), so no zero-init
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+constexpr uint32_t kQuadNext1 = 0x39;  // quad_perm [1,2,3,0]: column q+1
+constexpr uint32_t kQuadNext2 = 0x4E;  // [2,3,0,1]: column q+2
+constexpr uint32_t kQuadNext3 = 0x93;  // [3,0,1,2]: column q+3
+
+template <int NR, int COPIES>
+__device__ __forceinline__ uint32_t aes_encrypt_quad(uint32_t s, const Tab<COPIES>& T, const uint32_t (&k)[NR + 1]) {
+    s ^= k[0];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t s1 = quad_mov<kQuadNext1>(s), s2 = quad_mov<kQuadNext2>(s), s3 = quad_mov<kQuadNext3>(s);
+        if constexpr (COPIES == 16)
+            s = xor3(xor3(T.template get4<3, 0>(s), T.template get4<2, 1>(s1), T.template get4<1, 2>(s2)),
+                     T.template get4<0, 3>(s3), k[r]);
+        else
+            s = xor3(xor3(T.template get<3>(s), ror(T.template get<2>(s1), 8), ror(T.template get<1>(s2), 16)),
+                     ror(T.template get<0>(s3), 24), k[r]);
+    }
+    const uint32_t s1 = quad_mov<kQuadNext1>(s), s2 = quad_mov<kQuadNext2>(s), s3 = quad_mov<kQuadNext3>(s);
+    return xor3(xor3((T.template get<3>(s) << 8) & 0xFF000000u, T.template get<2>(s1) & 0x00FF0000u,
+                     T.template get<1>(s2) & 0x0000FF00u),
+                (T.template get<0>(s3) >> 8) & 0xFFu, k[NR]);
+}
+
+// big-endian word q of block blk of the virtual record [prefix][src][padding], byte by byte
+__device__ __forceinline__ uint32_t gather_word(const uint8_t* p, uint32_t len, uint32_t plen, uint32_t prefix,
+                                                uint32_t blk, uint32_t q) {
+    const uint32_t tot = len + plen, pad = 16 - (tot & 15);
+    uint32_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t k = 16 * blk + 4 * q + j;
+        uint32_t b;
+        if (k < plen)
+            b = (prefix >> (24 - 8 * k)) & 255u;
+        else if (k < tot)
+            b = p[k - plen];
+        else
+            b = pad;
+        word = (word << 8) | b;
+    }
+    return word;
+}
+
+__device__ __forceinline__ uint32_t load_be32(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);  // unaligned global_load_dword
+    return __builtin_bswap32(v);
+}
+
+// PRIO: waves whose records are long raise their issue priority, so the longest serial chains
+// (which set the kernel's floor) are not slowed by the short-record waves sharing their SIMD.
+template <int NR, int COPIES, int THREADS, bool PRIO = false>
+__global__ __launch_bounds__(THREADS) void aes_cbc_encrypt_quad_kernel(AesEncArgs a) {
+    __shared__ uint32_t lte[tab_words<COPIES>()];
+    fill_table<COPIES>(lte, a.te0, THREADS);
+    __syncthreads();
+    const Tab<COPIES> T{lte, lane_off<COPIES>()};
+    const uint64_t n = rec_count(a.count, a.n_max);
+    const uint64_t i = ((uint64_t)blockIdx.x * THREADS + threadIdx.x) >> 2;  // whole quads exit together
+    if (i >= n) return;
+    const uint32_t q = threadIdx.x & 3;
+    uint32_t k[NR + 1];
+#pragma unroll
+    for (int r = 0; r <= NR; r++)
+        k[r] = q == 0 ? a.rk[4 * r] : q == 1 ? a.rk[4 * r + 1] : q == 2 ? a.rk[4 * r + 2] : a.rk[4 * r + 3];
+    const uint32_t r = a.tasks ? a.tasks[i] : (uint32_t)i;
+    const uint8_t* p = a.src + a.src_off[r];
+    const uint32_t len = a.src_len[r];
+    const uint32_t plen = a.plen;
+    uint8_t* o = a.out + a.dst_off[r];
+    const uint32_t nfull = (len + plen) >> 4;
+    if constexpr (PRIO) {
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(nfull);
+        if (nb > 1536)
+            __builtin_amdgcn_s_setprio(3);
+        else if (nb > 1024)
+            __builtin_amdgcn_s_setprio(2);
+        else if (nb > 512)
+            __builtin_amdgcn_s_setprio(1);
+    }
+    uint32_t c = a.ivs ? load_be32(a.ivs + 16ull * r + 4 * q)
+                       : (q == 0 ? a.iv[0] : q == 1 ? a.iv[1] : q == 2 ? a.iv[2] : a.iv[3]);
+    uint32_t nx = 0;
+    if (nfull) nx = plen ? gather_word(p, len, plen, a.prefix, 0, q) : load_be32(p + 4 * q);
+    for (uint32_t b = 0; b < nfull; b++) {
+        const uint32_t x = nx ^ c;
+        const uint32_t bn = b + 1 < nfull ? b + 1 : b;
+        if (bn >= 1) nx = load_be32(p + 16ull * bn + 4 * q - plen);
+        c = aes_encrypt_quad<NR>(x, T, k);
+        const uint32_t be = __builtin_bswap32(c);
+        __builtin_memcpy(o + 16ull * b + 4 * q, &be, 4);
+    }
+    c = aes_encrypt_quad<NR>(gather_word(p, len, plen, a.prefix, nfull, q) ^ c, T, k);
+    const uint32_t be = __builtin_bswap32(c);
+    __builtin_memcpy(o + 16ull * nfull + 4 * q, &be, 4);
+    if (q == 0) a.dst_len[r] = 16 * (nfull + 1);
+}
+
 // ---- longest-first schedule (histogram of block counts, descending prefix, scatter)
 __global__ __launch_bounds__(256) void aes_hist_kernel(AesPlanArgs a) {
     __shared__ uint32_t lh[kAesBins];
@@ -483,7 +610,7 @@ struct sdfs_cdc_aes {
     int device = 0;
     int nr = 14;
     int num_cus = 256;
-    int enc_variant = 0;
+    int enc_variant = 7;  // quad form, 64 table copies, priority (SDFS_AES_VARIANT for A/B)
     uint32_t rk[60];
     uint32_t dk[60];
     hipStream_t stream = nullptr;
@@ -512,11 +639,35 @@ void launch_enc(uint64_t n_max, const AesEncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((aes_cbc_encrypt_kernel<NR, COPIES, THREADS>), dim3(g), dim3(THREADS), 0, s, a);
 }
 
+template <int NR, int COPIES, int THREADS, bool PRIO = false>
+void launch_enc_quad(uint64_t n_max, const AesEncArgs& a, hipStream_t s) {
+    const uint32_t g = (uint32_t)((4 * n_max + THREADS - 1) / THREADS);
+    hipLaunchKernelGGL((aes_cbc_encrypt_quad_kernel<NR, COPIES, THREADS, PRIO>), dim3(g), dim3(THREADS), 0, s, a);
+}
+
 // variant 0: 32 table copies (32 KiB), 256-thread workgroups (5 per CU); 1: 64 copies with the
-// one-v_perm index (64 KiB), 512 threads (2 per CU); 2: 64 copies, 256 threads.
+// one-v_perm index (64 KiB), 512 threads (2 per CU); 2: 64 copies, 256 threads; 3/4: the quad
+// form (4 lanes per record) with 64 / 32 copies, 256 threads; 5: quad, 64 copies, 1024 threads;
+// 6 / 7: variants 4 / 3 with issue priority for waves of long records; 8: quad + priority with
+// the four rotated tables (no v_alignbit, 2-way bank conflicts); 9: quad + priority, 64 copies,
+// 512 threads.
 template <int NR>
 void launch_encrypt_nr(int variant, uint64_t n_max, const AesEncArgs& a, hipStream_t s) {
-    if (variant == 1)
+    if (variant == 3)
+        launch_enc_quad<NR, 64, 256>(n_max, a, s);
+    else if (variant == 5)
+        launch_enc_quad<NR, 64, 1024>(n_max, a, s);
+    else if (variant == 6)
+        launch_enc_quad<NR, 32, 256, true>(n_max, a, s);
+    else if (variant == 7)
+        launch_enc_quad<NR, 64, 256, true>(n_max, a, s);
+    else if (variant == 8)
+        launch_enc_quad<NR, 16, 256, true>(n_max, a, s);
+    else if (variant == 9)
+        launch_enc_quad<NR, 64, 512, true>(n_max, a, s);
+    else if (variant == 4)
+        launch_enc_quad<NR, 32, 256>(n_max, a, s);
+    else if (variant == 1)
         launch_enc<NR, 64, 512>(n_max, a, s);
     else if (variant == 2)
         launch_enc<NR, 64, 256>(n_max, a, s);

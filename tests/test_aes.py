@@ -273,3 +273,28 @@ def test_gpu_lz4_then_aes_chain():
         want = A.cbc_encrypt(key, iv, rec)
         assert a[aoff[i]: aoff[i] + al[i]].tobytes() == want, i
     z.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+def test_gpu_encrypt_variants_agree(variant, monkeypatch):
+    """Every kernel layout (table copies, lane-per-record or quad-per-record) gives the oracle's bytes."""
+    from sdfs_amd.aes import HipEncryptUtils
+
+    monkeypatch.setenv("SDFS_AES_VARIANT", str(variant))
+    key = _key(32, 9)
+    c = HipEncryptUtils(key)
+    rng = np.random.default_rng(20 + variant)
+    lens = [int(x) for x in rng.integers(0, 34000, 300)] + LENS
+    datas = [C.synth(8, i, 0, n).tobytes() for i, n in enumerate(lens)]
+    offs = np.concatenate([[0], np.cumsum([len(d) + 1 for d in datas[:-1]])]).astype(np.uint64)
+    base = np.zeros(int(offs[-1]) + len(datas[-1]) + 8, np.uint8)
+    for o, d in zip(offs, datas):
+        base[int(o): int(o) + len(d)] = np.frombuffer(d, np.uint8)
+    iv = bytes(range(50, 66))
+    for prefix in (None, -1):
+        pre = b"" if prefix is None else struct.pack(">i", prefix)
+        outs = c.encrypt_chunks(base, offs, lens, iv, nz_prefix=prefix)
+        for d, out in zip(datas, outs):
+            assert out == A.cbc_encrypt(key, iv, d, prefix=pre)
+    c.destroy()
