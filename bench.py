@@ -82,7 +82,7 @@ def main():
 
     from sdfs_amd import HipVariableSha256HashEngine, SdfsConfig
     from sdfs_amd.device import DeviceBatch
-    from sdfs_amd.dist import allgather_records, shard_streams
+    from sdfs_amd.dist import RecordExchange, shard_streams
 
     cfg = SdfsConfig(chunk_length=args.buf_kib * 1024)
     eng = HipVariableSha256HashEngine(config=cfg, device=local)
@@ -94,16 +94,24 @@ def main():
     batch.fill_streams(first_stream=streams.start, bufs_per_stream=bufs_per_stream)
     torch.cuda.synchronize()
     cs = torch.cuda.current_stream()
+    # N > 1: the one real exchange (all-gather of the fingerprint records), pipelined on a side
+    # stream so step i's tables travel while step i+1 is chunked (sdfs_amd/dist.py)
+    ex = RecordExchange(batch.recs.view(-1, 48).shape[0], f"cuda:{local}") if world > 1 else None
     gathered = [0]
 
     def step():
         batch.run(buffer_id_base=rank * nbuf, stream=cs.cuda_stream)
-        if world > 1:
-            g = allgather_records(batch.recs.view(-1, 48), batch.total)
-            gathered[0] = g.shape[0]
+        if ex is not None:
+            ex.submit(batch.recs.view(-1, 48), batch.total, stream=cs)
+
+    def drain():
+        if ex is not None:
+            res = ex.flush()
+            gathered[0] = sum(cl for _, counts in res[-1:] for cl in counts)
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -113,6 +121,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:

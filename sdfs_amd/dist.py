@@ -8,8 +8,15 @@ backend is RCCL over xGMI; the same code runs on "gloo" for CPU tests.
 
 Protocol: all-gather the record counts (one int64 per rank), then all-gather the tables padded
 to the largest count (all_gather_into_tensor needs equal sizes), then drop the padding.
+
+:class:`RecordExchange` runs that protocol pipelined for a stream of batches: batch i's table is
+snapshotted on the producer stream and exchanged on a side stream while batch i+1 is being
+chunked, so on N GPUs the exchange overlaps compute instead of adding to every step (SURVEY.md
+8(e): ~24 MiB per GPU per step over xGMI).
 """
 from __future__ import annotations
+
+from collections import deque
 
 import torch
 import torch.distributed as dist
@@ -44,3 +51,94 @@ def allgather_records(table: torch.Tensor, count: int | torch.Tensor, group=None
     dist.all_gather_into_tensor(gathered, local.contiguous(), group=group)
     parts = [gathered[r * mx: r * mx + cl[r]] for r in range(world)]
     return torch.cat(parts, 0)
+
+
+class RecordExchange:
+    """Pipelined all-gather of per-step fingerprint tables.
+
+    ``submit(table, count)`` snapshots ``table[:capacity]`` and the device ``count`` on the
+    producer stream (no host sync) and starts the count all-gather on a side stream; the table
+    all-gather of a step is issued when the pipeline is ``depth`` steps deep (or on ``flush``),
+    after its counts are known on the side stream.  The producer stream only waits for a slot's
+    previous exchange before overwriting it.  Results are ``(gathered, counts)``: gathered is
+    [world * max(counts), 48] in rank order, rank r's rows at [r * max, r * max + counts[r]).
+    On CPU tensors (gloo) every call is synchronous.
+    """
+
+    def __init__(self, capacity: int, device, group=None, depth: int = 2):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.capacity = int(capacity)
+        self.depth = max(1, int(depth))
+        self.slots = [torch.empty(self.capacity, RECORD_BYTES, dtype=torch.uint8, device=self.device)
+                      for _ in range(self.depth)]
+        self.cnt = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.depth)]
+        self.counts = [torch.zeros(self.world, dtype=torch.int64, device=self.device) for _ in range(self.depth)]
+        self.free = [None] * self.depth  # side-stream event after a slot's table all-gather
+        self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        self.pending = deque()
+        self.results = []
+        self.n = 0
+
+    def _ctx(self):
+        import contextlib
+        return torch.cuda.stream(self.side) if self.cuda else contextlib.nullcontext()
+
+    def submit(self, table: torch.Tensor, count, stream=None) -> None:
+        if len(self.pending) == self.depth:
+            self.results.append(self._finish(self.pending.popleft()))
+        slot = self.n % self.depth
+        self.n += 1
+        prod = None
+        if self.cuda:
+            prod = stream if stream is not None else torch.cuda.current_stream(self.device)
+            if not isinstance(prod, torch.cuda.Stream):
+                prod = torch.cuda.ExternalStream(prod, device=self.device)
+            if self.free[slot] is not None:
+                prod.wait_event(self.free[slot])
+        n = min(self.capacity, table.shape[0])
+        c = count if isinstance(count, torch.Tensor) else torch.tensor([count], device=self.device)
+        if self.cuda:
+            with torch.cuda.stream(prod):
+                self.slots[slot][:n].copy_(table[:n], non_blocking=True)
+                self.cnt[slot].copy_(c.reshape(1).to(torch.int64), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(prod)
+            self.side.wait_event(ev)
+        else:
+            self.slots[slot][:n].copy_(table[:n])
+            self.cnt[slot].copy_(c.reshape(1).to(torch.int64))
+        with self._ctx():
+            dist.all_gather_into_tensor(self.counts[slot], self.cnt[slot], group=self.group)
+        self.pending.append(slot)
+
+    def _finish(self, slot: int):
+        with self._ctx():
+            cl = self.counts[slot].tolist()  # syncs the side stream only
+            if max(cl) > self.capacity:
+                raise ValueError(f"record count {max(cl)} exceeds the exchange capacity {self.capacity}")
+            mx = max(cl) if cl else 0
+            gathered = torch.empty(self.world * mx, RECORD_BYTES, dtype=torch.uint8, device=self.device)
+            if mx:
+                dist.all_gather_into_tensor(gathered, self.slots[slot][:mx], group=self.group)
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+                self.free[slot] = ev
+        return gathered, cl
+
+    def flush(self) -> list:
+        """Finish every pending step; returns (and clears) all results in submission order."""
+        while self.pending:
+            self.results.append(self._finish(self.pending.popleft()))
+        out, self.results = self.results, []
+        return out
+
+    @staticmethod
+    def compact(gathered: torch.Tensor, counts) -> torch.Tensor:
+        """Drop the padding: [sum(counts), 48] in rank order."""
+        mx = max(counts) if counts else 0
+        return torch.cat([gathered[r * mx: r * mx + c] for r, c in enumerate(counts)], 0) if mx else \
+            gathered.new_empty((0, RECORD_BYTES))

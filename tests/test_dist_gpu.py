@@ -1,0 +1,50 @@
+"""The pipelined record exchange on the GPU (RCCL, world size 1 on the one-GPU test box): the CUDA
+stream/event handling of sdfs_amd.dist.RecordExchange that bench.py runs at N > 1.  World size
+2-3 over gloo is covered on CPU by tests/test_dist.py; N = 8 over xGMI is the driver's run."""
+import os
+import socket
+
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_record_exchange_rccl_world1_overlapped_steps():
+    import torch
+    import torch.distributed as dist
+
+    from sdfs_amd import HipVariableSha256HashEngine
+    from sdfs_amd.device import DeviceBatch
+    from sdfs_amd.dist import RecordExchange
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        eng = HipVariableSha256HashEngine()
+        batch = DeviceBatch(eng, nbuf=64, buf_len=262144)
+        ex = RecordExchange(batch.recs.view(-1, 48).shape[0], "cuda:0", depth=2)
+        cs = torch.cuda.current_stream()
+        want = []
+        for step in range(5):  # no host sync between steps: the exchange overlaps the next step
+            batch.fill_streams(first_stream=10 * step, bufs_per_stream=8)
+            batch.run(buffer_id_base=0, stream=cs.cuda_stream)
+            ex.submit(batch.recs.view(-1, 48), batch.total, stream=cs)
+            want.append((batch.recs.view(-1, 48).clone(), batch.total.clone()))  # stream-ordered copy
+        got = ex.flush()
+        torch.cuda.synchronize()
+        assert len(got) == 5
+        for (g, cl), (wt, wn) in zip(got, want):
+            n = int(wn.item())
+            assert cl == [n] and n > 0
+            assert torch.equal(RecordExchange.compact(g, cl), wt[:n])
+        eng.destroy()
+    finally:
+        dist.destroy_process_group()
