@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--cpu-secs", type=float, default=12.0, help="CPU baseline sample size (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e-mib", type=int, default=1024, help="host->GPU->host measurement size (0 = skip)")
+    ap.add_argument("--exchange", type=int, default=-1,
+                    help="record all-gather: -1 = when N > 1, 1 = also at N = 1 (exercises the path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -77,7 +79,13 @@ def main():
     import torch.distributed as dist
 
     torch.cuda.set_device(local)
-    if world > 1:
+    use_ex = world > 1 if args.exchange < 0 else bool(args.exchange)
+    if use_ex:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
     from sdfs_amd import HipVariableSha256HashEngine, SdfsConfig
@@ -96,7 +104,7 @@ def main():
     cs = torch.cuda.current_stream()
     # N > 1: the one real exchange (all-gather of the fingerprint records), pipelined on a side
     # stream so step i's tables travel while step i+1 is chunked (sdfs_amd/dist.py)
-    ex = RecordExchange(batch.recs.view(-1, 48).shape[0], f"cuda:{local}") if world > 1 else None
+    ex = RecordExchange(batch.recs.view(-1, 48).shape[0], f"cuda:{local}") if use_ex else None
     gathered = [0]
 
     def step():
@@ -158,7 +166,7 @@ def main():
         e2e = nb * buf_len * reps / (time.perf_counter() - te) / 2**30
 
     if rank != 0:
-        if world > 1:
+        if use_ex:
             dist.destroy_process_group()
         return
 
@@ -194,7 +202,7 @@ def main():
             "params": "P=0x26CE86126EF863 W=48 minLen=4095 maxLen=32768 pred=(fp&0xFFF)==0 n>minLen SHA-256",
             "mean_chunk_bytes": round(nbytes / max(total, 1), 1),
             "chunks_per_gpu_step": total,
-            "exchange": "RCCL all_gather of 48-B fingerprint records" if world > 1 else "none (N=1)",
+            "exchange": "RCCL all_gather of 48-B fingerprint records, pipelined" if use_ex else "none (N=1)",
             "parallelism": f"dp{world} (streams sharded per GPU)",
         },
         "kernels_ms": {k: round(v, 4) for k, v in kt.items()},
@@ -215,7 +223,7 @@ def main():
         "e2e_host_gibps": round(e2e, 3) if e2e else None,
     }
     print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_ex:
         dist.destroy_process_group()
 
 
