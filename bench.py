@@ -68,6 +68,10 @@ def main():
     ap.add_argument("--cpu-secs", type=float, default=12.0, help="CPU baseline sample size (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e-mib", type=int, default=1024, help="host->GPU->host measurement size (0 = skip)")
+    ap.add_argument("--min-seg-kib", type=int, default=4,
+                    help="min-variable-segment-size (minLen = KiB*1024-1; 4 = the reference default)")
+    ap.add_argument("--mask-bits", type=int, default=12,
+                    help="boundary predicate (fp & (2^bits-1)) == 0 (12 = the default knob, SURVEY.md A.3)")
     ap.add_argument("--exchange", type=int, default=-1,
                     help="record all-gather: -1 = when N > 1, 1 = also at N = 1 (exercises the path)")
     args = ap.parse_args()
@@ -92,7 +96,8 @@ def main():
     from sdfs_amd.device import DeviceBatch
     from sdfs_amd.dist import RecordExchange, shard_streams
 
-    cfg = SdfsConfig(chunk_length=args.buf_kib * 1024)
+    cfg = SdfsConfig(chunk_length=args.buf_kib * 1024, min_len=args.min_seg_kib * 1024 - 1,
+                     pred_mask=(1 << args.mask_bits) - 1)
     eng = HipVariableSha256HashEngine(config=cfg, device=local)
     buf_len = args.buf_kib * 1024
     bufs_per_stream = args.stream_mib * 1024 // args.buf_kib
@@ -199,7 +204,8 @@ def main():
         "config": {
             "workload": f"{args.streams} streams x {args.stream_mib} MiB per GPU, CHUNK_LENGTH {buf_len} B "
                         f"({nbuf} buffers, {nbytes / 2**30:.2f} GiB per GPU), fresh CDC state per buffer",
-            "params": "P=0x26CE86126EF863 W=48 minLen=4095 maxLen=32768 pred=(fp&0xFFF)==0 n>minLen SHA-256",
+            "params": f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
+                      f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen SHA-256",
             "mean_chunk_bytes": round(nbytes / max(total, 1), 1),
             "chunks_per_gpu_step": total,
             "exchange": "RCCL all_gather of 48-B fingerprint records, pipelined" if use_ex else "none (N=1)",
