@@ -1214,9 +1214,10 @@ __device__ __forceinline__ void md5_compress(uint32_t (&s)[4], const uint32_t (&
 // hold at least one chunk byte are read.
 template <bool SHA>
 __device__ __forceinline__ void tail_words(uint32_t (&m)[16], const uint8_t* t, uint32_t rem) {
-    const uintptr_t ta = reinterpret_cast<uintptr_t>(t);
-    const uint32_t r = (uint32_t)(ta & 3);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(ta - r);
+    const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(t) & 3);
+    // pointer arithmetic (not an integer round trip) keeps the global address space: global_load,
+    // not flat_load
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(t - r);
     const uint32_t nd = (r + rem + 3) >> 2;
     uint32_t d[17];
 #pragma unroll

@@ -49,6 +49,10 @@ struct Lz4Args {
     uint32_t framed;
 };
 
+// LDS byte scratch accessed as volatile LDS (ds_write_b8 / ds_read_u8, ordered per wave): a
+// volatile GENERIC pointer would become flat accesses with system-scope bits and vmcnt(0) waits.
+typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
+
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
     uint32_t v;
     __builtin_memcpy(&v, p, 4);
@@ -148,7 +152,7 @@ __device__ __forceinline__ uint32_t match_count(const uint8_t* src, uint32_t a0,
 // One chunk, one wave (all lanes run the same scalar control flow).  Returns the block length.
 template <int MODE>
 __device__ uint32_t compress_chunk(const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ dst,
-                                   uint32_t* tab, volatile uint8_t* scr, uint32_t lane) {
+                                   uint32_t* tab, lds_vu8* scr, uint32_t lane) {
     {
         uint4* t4 = reinterpret_cast<uint4*>(tab);
         for (uint32_t i = lane; i < 1024; i += 64) t4[i] = make_uint4(0, 0, 0, 0);
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(Lz4Args a) {
         const uint32_t n = a.src_len[c];
         uint8_t* o = a.out + a.dst_off[c];
         const uint32_t hdr = a.framed ? 4u : 0u;
-        const uint32_t len = compress_chunk<MODE>(a.data + a.src_off[c], n, o + hdr, tab, scr, lane);
+        const uint32_t len = compress_chunk<MODE>(a.data + a.src_off[c], n, o + hdr, tab, (lds_vu8*)scr, lane);
         if (lane == 0) {
             if (hdr) {
                 o[0] = (uint8_t)(n >> 24);
