@@ -112,6 +112,18 @@ uint32_t sdfs_cdc_slot_cap(const sdfs_cdc_engine* e, uint64_t buf_len);
  * Host bytes in, digest_len bytes out (computed on the GPU). */
 int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest);
 
+/* ---- getHash in bulk: many chunks fingerprinted in one GPU pass ----
+ * The getHash callers that verify or key whole chunks (HashBlobArchive.java:1271-1276 VERIFY_WRITES,
+ * :1936-1940 VERIFY_READS; HashStore.java:63-71; WritableCacheBuffer.java:93-97) one call per chunk
+ * today.  Host form: chunk i = base[offs[i] .. + lens[i]) (each < 4 GiB), digest_len bytes per
+ * chunk written densely to digests.  Device form: chunk i (i < *d_count when d_count != NULL,
+ * else i < n_max) = d_data[d_offs[i] .. + d_lens[i]), 32-byte digest slot i of d_digests
+ * (digest_len bytes used, zero-padded); chunks are scheduled longest first; enqueued on stream. */
+int sdfs_cdc_get_hash_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
+                            uint32_t n, uint8_t* digests);
+int sdfs_cdc_hash_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
+                         const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, void* stream);
+
 /* ---- AbstractHashEngine.getChunks(byte[], uuid) (VariableSha256HashEngine.java:71-86) ----
  * One host buffer (1..CHUNK_LENGTH bytes, fresh CDC state).  Writes *count chunks into
  * starts/lens/digests (digest_len bytes each, densely packed), capacity cap entries. */

@@ -240,6 +240,11 @@ struct sdfs_cdc_engine {
     DevBuf<uint8_t> h_data;
     DevBuf<uint32_t> o_starts;
     DevBuf<uint8_t> o_digests;
+    DevBuf<uint32_t> x_scratch;  // extent ordering: hist | cursor | total, then starts | tasks
+    DevBuf<uint8_t> x_data;      // host-batch staging of getHash in bulk
+    DevBuf<uint64_t> x_offs;
+    DevBuf<uint32_t> x_lens;
+    DevBuf<uint8_t> x_digests;
     uint8_t* pin_data = nullptr;
     size_t pin_data_n = 0;
     // batched host path: two slots, H2D on its own stream, packing on copy_threads threads
@@ -788,6 +793,11 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
         e->h_data.release();
         e->o_starts.release();
         e->o_digests.release();
+        e->x_scratch.release();
+        e->x_data.release();
+        e->x_offs.release();
+        e->x_lens.release();
+        e->x_digests.release();
         if (e->pin_data) (void)hipHostFree(e->pin_data);
         if (e->s_h2d) (void)hipStreamSynchronize(e->s_h2d);
         for (auto& sl : e->hs) {
@@ -960,6 +970,80 @@ int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uin
     HIP_TRY(hipMemcpyAsync(ctl + 4, e->o_digests.p, 32, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     memcpy(digest, ctl + 4, e->digest_len);
+    return SDFS_CDC_OK;
+}
+
+namespace {
+// fingerprints of n extents on the engine (caller holds e->mu and has set the device)
+int hash_extents(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
+                 const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, hipStream_t s) {
+    if (n_max == 0) return SDFS_CDC_OK;
+    if (n_max > 0xFFFFFFFFull) return fail(SDFS_CDC_EINVAL, "more than 2^32 extents");
+    HIP_TRY(e->x_scratch.ensure(kExtentScratchWords + 2 * n_max));
+    uint32_t* sc = e->x_scratch.p;
+    ExtentArgs xa{d_lens, d_count, n_max, sc + kExtentScratchWords, sc + kExtentScratchWords + n_max,
+                  sc + 1024, sc, sc + 512};
+    HIP_TRY(launch_extent_order(xa, s));
+    HashArgs ha{};
+    ha.data = d_data;
+    ha.offs = d_offs;
+    ha.uniform_len = 0;
+    ha.tasks = xa.tasks;
+    ha.total = xa.total;
+    ha.starts = xa.starts;
+    ha.clens = d_lens;
+    ha.cap = 1;
+    ha.digests = d_digests;
+    ha.algo = e->prm.hash_algo;
+    HIP_TRY(launch_hash(ha, n_max, 0, s));
+    return SDFS_CDC_OK;
+}
+}  // namespace
+
+int sdfs_cdc_hash_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
+                         const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, void* stream) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    if (n_max && (!d_data || !d_offs || !d_lens || !d_digests)) return fail(SDFS_CDC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    return hash_extents(e, d_data, d_offs, d_lens, d_count, n_max, d_digests, reinterpret_cast<hipStream_t>(stream));
+}
+
+int sdfs_cdc_get_hash_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
+                            uint32_t n, uint8_t* digests) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    if (n == 0) return SDFS_CDC_OK;
+    if (!base || !offs || !lens || !digests) return fail(SDFS_CDC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->prm.device));
+    hipStream_t s = e->stream;
+    // pack the chunks 16-byte aligned into pinned staging, one H2D
+    std::vector<uint64_t> po(n);
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        po[i] = bytes;
+        bytes += (lens[i] + 15ull) & ~15ull;
+    }
+    int rc = pinned_ensure(&e->pin_data, &e->pin_data_n, bytes + 64);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n; i++) memcpy(e->pin_data + po[i], base + offs[i], lens[i]);
+    HIP_TRY(e->x_data.ensure(bytes + 64));
+    HIP_TRY(e->x_offs.ensure(n));
+    HIP_TRY(e->x_lens.ensure(n));
+    HIP_TRY(e->x_digests.ensure(32ull * n));
+    HIP_TRY(hipMemcpyAsync(e->x_data.p, e->pin_data, bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->x_offs.p, po.data(), 8ull * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->x_lens.p, lens, 4ull * n, hipMemcpyHostToDevice, s));
+    rc = hash_extents(e, e->x_data.p, e->x_offs.p, e->x_lens.p, nullptr, n, e->x_digests.p, s);
+    if (rc) {
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
+    std::vector<uint8_t> dg(32ull * n);
+    HIP_TRY(hipMemcpyAsync(dg.data(), e->x_digests.p, 32ull * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t dl = (uint32_t)e->digest_len;
+    for (uint32_t i = 0; i < n; i++) memcpy(digests + (uint64_t)dl * i, dg.data() + 32ull * i, dl);
     return SDFS_CDC_OK;
 }
 

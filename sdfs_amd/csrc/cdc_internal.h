@@ -123,6 +123,20 @@ struct HashArgs {
     uint32_t* wave_ctr;        // [1] zeroed task counter of the persistent variant
 };
 
+// Longest-first order of arbitrary chunk extents (getHash in bulk): tasks[] = extent indices,
+// starts[] zeroed, *total = the live count.  hist/cursor: 512 words each (engine scratch).
+struct ExtentArgs {
+    const uint32_t* lens;
+    const uint32_t* count;  // optional device count (else n_max)
+    uint64_t n_max;
+    uint32_t* starts;
+    uint32_t* tasks;
+    uint32_t* total;
+    uint32_t* hist;
+    uint32_t* cursor;
+};
+constexpr uint32_t kExtentScratchWords = 2 * 512 + 1;
+
 // Record a C-ABI error message (sdfs_cdc_last_error) and return `code`.
 int fail_status(int code, const char* fmt, ...);
 
@@ -141,6 +155,7 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);
 hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);
+hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t stream);
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
                         hipStream_t stream);
 bool scan_window_supported(int window);

@@ -1450,6 +1450,80 @@ __global__ __launch_bounds__(256) void synth_kernel(uint8_t* out, uint64_t n, ui
     }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// 6. fingerprints of given extents (getHash in bulk): longest-first order of n chunk lengths
+// ------------------------------------------------------------------------------------------
+// bin = sha_blocks(len) >> 2, capped: 4-block bins up to 2048 blocks (128 KiB), then one bin.
+constexpr uint32_t kExtBins = 512, kExtShift = 2;
+
+__device__ __forceinline__ uint32_t ext_count(const uint32_t* count, uint64_t n_max) {
+    return count ? (uint32_t)min<uint64_t>(*count, n_max) : (uint32_t)n_max;
+}
+__device__ __forceinline__ uint32_t ext_bin(uint32_t len) {
+    const uint32_t b = sha_blocks(len) >> kExtShift;
+    return b < kExtBins ? b : kExtBins - 1;
+}
+
+__global__ __launch_bounds__(256) void ext_hist_kernel(ExtentArgs a) {
+    __shared__ uint32_t lh[kExtBins];
+    for (uint32_t k = threadIdx.x; k < kExtBins; k += 256) lh[k] = 0;
+    __syncthreads();
+    const uint32_t n = ext_count(a.count, a.n_max);
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        atomicAdd(&lh[ext_bin(a.lens[i])], 1u);
+        a.starts[i] = 0;  // every extent is its own "buffer" with one slot at offset 0
+    }
+    if (i == 0) *a.total = n;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kExtBins; k += 256)
+        if (lh[k]) atomicAdd(&a.hist[k], lh[k]);
+}
+
+__global__ __launch_bounds__(kExtBins) void ext_cursor_kernel(ExtentArgs a) {
+    __shared__ uint32_t part[kExtBins];
+    const uint32_t t = threadIdx.x;
+    part[t] = a.hist[kExtBins - 1 - t];  // longest bin first
+    __syncthreads();
+    for (uint32_t d = 1; d < kExtBins; d <<= 1) {
+        const uint32_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    a.cursor[kExtBins - 1 - t] = part[t] - a.hist[kExtBins - 1 - t];
+}
+
+__global__ __launch_bounds__(256) void ext_scatter_kernel(ExtentArgs a) {
+    __shared__ uint32_t lc[kExtBins], lb[kExtBins];
+    for (uint32_t k = threadIdx.x; k < kExtBins; k += 256) lc[k] = 0;
+    __syncthreads();
+    const uint32_t n = ext_count(a.count, a.n_max);
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t bin = 0, rank = 0;
+    if (i < n) {
+        bin = ext_bin(a.lens[i]);
+        rank = atomicAdd(&lc[bin], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kExtBins; k += 256)
+        if (lc[k]) lb[k] = atomicAdd(&a.cursor[k], lc[k]);
+    __syncthreads();
+    if (i < n) a.tasks[lb[bin] + rank] = (uint32_t)i;
+}
+
+hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t s) {
+    if (a.n_max == 0) return hipSuccess;
+    const uint32_t g = (uint32_t)((a.n_max + 255) / 256);
+    hipError_t e = hipMemsetAsync(a.hist, 0, kExtBins * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ext_hist_kernel, dim3(g), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(ext_cursor_kernel, dim3(1), dim3(kExtBins), 0, s, a);
+    hipLaunchKernelGGL(ext_scatter_kernel, dim3(g), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
                         hipStream_t s) {
     if (n == 0) return hipSuccess;

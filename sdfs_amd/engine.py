@@ -175,6 +175,32 @@ class HipVariableSha256HashEngine:
         check(self._lib.sdfs_cdc_get_hash(self._h, ptr, len(a), out))
         return bytes(out)[: self.digest_len]
 
+    def getHashes(self, chunks) -> list:
+        """getHash over many chunks in one GPU pass (sdfs_cdc_get_hash_batch)."""
+        import numpy as np
+
+        chunks = [bytes(c) for c in chunks]
+        n = len(chunks)
+        if n == 0:
+            return []
+        lens = np.array([len(c) for c in chunks], np.uint32)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+        base = np.frombuffer(b"".join(chunks) or b"\0", np.uint8)
+        out = np.zeros(n * self.digest_len, np.uint8)
+        check(self._lib.sdfs_cdc_get_hash_batch(self._h, base.ctypes.data, offs.ctypes.data, lens.ctypes.data, n,
+                                                out.ctypes.data))
+        return [out[i * self.digest_len:(i + 1) * self.digest_len].tobytes() for i in range(n)]
+
+    def hash_device(self, data, offs, lens, digests, count=None, stream=None) -> None:
+        """Device tensors: data u8, offs i64[n], lens i32[n], digests u8[n, 32] (written)."""
+        import torch
+
+        n = int(lens.shape[0])
+        s = stream if stream is not None else torch.cuda.current_stream(data.device).cuda_stream
+        check(self._lib.sdfs_cdc_hash_device(self._h, data.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                             count.data_ptr() if count is not None else None, n,
+                                             digests.data_ptr(), s))
+
     def setSeed(self, seed: int) -> None:  # no-op in variable engines (:116-120)
         check(self._lib.sdfs_cdc_set_seed(self._h, int(seed)))
 

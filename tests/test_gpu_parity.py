@@ -338,3 +338,42 @@ def test_device_error_paths_raise():
         e.run_device(batch.data.data_ptr(), 2, 262144, bad)
     with pytest.raises(_lib.SdfsCdcError):
         e.run_device(batch.data.data_ptr() + 1, 2, 262144, batch.out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["sha256", "sha256_160", "md5"])
+def test_get_hash_batch_and_device_extents(algo):
+    """getHash in bulk (sdfs_cdc_get_hash_batch / sdfs_cdc_hash_device) == hashlib, order kept."""
+    import hashlib
+
+    import numpy as np
+    import torch
+
+    from sdfs_amd import HipVariableMD5HashEngine, HipVariableSha256HashEngine
+    e = (HipVariableMD5HashEngine() if algo == "md5" else
+         HipVariableSha256HashEngine(HipVariableSha256HashEngine.HASH160 if algo == "sha256_160"
+                                     else HipVariableSha256HashEngine.HASH256))
+    hf = (lambda b: hashlib.md5(b).digest()) if algo == "md5" else (lambda b: hashlib.sha256(b).digest())
+    dl = 16 if algo == "md5" else (20 if algo == "sha256_160" else 32)
+    rng = np.random.default_rng(31)
+    lens = [int(x) for x in rng.integers(0, 40000, 500)] + [0, 1, 55, 56, 63, 64, 65, 119, 120, 131072, 300000]
+    chunks = [O.synth(12, i, 0, n).tobytes() for i, n in enumerate(lens)]
+    got = e.getHashes(chunks)
+    assert [g for g in got] == [hf(c)[:dl] for c in chunks]
+    # device form, unaligned offsets, device count
+    offs = np.concatenate([[1], 1 + np.cumsum([len(c) + 3 for c in chunks[:-1]])]).astype(np.int64)
+    base = np.zeros(int(offs[-1]) + len(chunks[-1]) + 8, np.uint8)
+    for o, c in zip(offs, chunks):
+        base[int(o): int(o) + len(c)] = np.frombuffer(c, np.uint8)
+    dev = torch.device("cuda:0")
+    d = torch.from_numpy(base).to(dev)
+    dg = torch.zeros(len(chunks), 32, dtype=torch.uint8, device=dev)
+    k = len(chunks) - 7
+    e.hash_device(d, torch.from_numpy(offs).to(dev), torch.tensor(lens, dtype=torch.int32, device=dev), dg,
+                  count=torch.tensor([k], dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    out = dg.cpu().numpy()
+    for i in range(k):
+        assert out[i, :dl].tobytes() == hf(chunks[i])[:dl], i
+    assert not out[k:].any()
+    e.destroy()
