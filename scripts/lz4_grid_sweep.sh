@@ -1,0 +1,1 @@
+for k in 2 4 6 8 9 12; do SDFS_LZ4_WG_PER_CU=$k SETS=text,random MODES=r123 REPS=3 NBUF=1024 CPU_SECS=0 THREADS=2 python scripts/lz4_bench.py | sed "s/^{/{\"wg_per_cu\": $k, /"; done

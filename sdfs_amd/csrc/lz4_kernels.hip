@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -35,7 +36,8 @@ constexpr uint32_t kMinMatch = 4, kMfLimit = 12, kLastLiterals = 5, kMlMask = 15
 constexpr uint32_t kLimit64K = 65536 + kMfLimit - 1;  // below: 16-bit position table
 constexpr uint32_t kMaxDistance = 65535;
 constexpr uint32_t kScrBuckets = 1024;  // same-entry detection among one round's 64 probes
-constexpr int kLz4WgPerCu = 8;          // 17 KiB of LDS per one-wave workgroup
+constexpr int kLz4WgPerCu = 9;          // 17 KiB of LDS per one-wave workgroup: 9 fit in 160 KiB
+                                        // (latency-bound: throughput ~ waves in flight, scripts/lz4_grid_sweep.sh)
 
 struct Lz4Args {
     const uint8_t* data;
@@ -450,6 +452,7 @@ struct sdfs_cdc_lz4 {
     int device = 0;
     int mode = SDFS_CDC_LZ4_R123;
     int num_cus = 256;
+    int wg_per_cu = kLz4WgPerCu;  // SDFS_LZ4_WG_PER_CU overrides (measurements)
     hipStream_t stream = nullptr;
     ZBuf<uint64_t> bsum;
     // host-path scratch
@@ -471,7 +474,7 @@ namespace {
 
 int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
     if (a.n_max == 0) return SDFS_CDC_OK;
-    const uint64_t grid = std::min<uint64_t>(a.n_max, (uint64_t)z->num_cus * kLz4WgPerCu);
+    const uint64_t grid = std::min<uint64_t>(a.n_max, (uint64_t)z->num_cus * z->wg_per_cu);
     if (z->mode == SDFS_CDC_LZ4_V19)
         hipLaunchKernelGGL(lz4_compress_kernel<SDFS_CDC_LZ4_V19>, dim3((uint32_t)grid), dim3(64), 0, s, a);
     else
@@ -503,6 +506,7 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     z->device = device;
     z->mode = mode;
     z->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (const char* v = getenv("SDFS_LZ4_WG_PER_CU")) z->wg_per_cu = std::max(1, atoi(v));
     if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
         delete z;
         return fail_status(SDFS_CDC_EHIP, "stream creation failed");
