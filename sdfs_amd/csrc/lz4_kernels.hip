@@ -49,6 +49,7 @@ struct Lz4Args {
     const uint64_t* dst_off;
     uint32_t* dst_len;
     uint32_t framed;
+    uint32_t* gtab;  // GTAB kernels: 16 KiB hash table per workgroup in global memory
 };
 
 // LDS byte scratch accessed as volatile LDS (ds_write_b8 / ds_read_u8, ordered per wave): a
@@ -305,10 +306,13 @@ __device__ uint32_t compress_chunk(const uint8_t* __restrict__ src, uint32_t n, 
 
 // One wave per workgroup; chunk c = blockIdx.x + k * gridDim.x (a static stride balances well:
 // hundreds of chunks per workgroup, and a shared counter would serialise ~10^6 dequeues).
-template <int MODE>
+// GTAB: the hash table lives in global memory (L2 / Infinity Cache) instead of LDS, so LDS no
+// longer caps the chunks in flight per CU (1 KiB of LDS per wave instead of 17 KiB).
+template <int MODE, bool GTAB = false>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(Lz4Args a) {
-    __shared__ __attribute__((aligned(16))) uint32_t tab[4096];
+    __shared__ __attribute__((aligned(16))) uint32_t ltab[GTAB ? 4 : 4096];
     __shared__ uint8_t scr[kScrBuckets];
+    uint32_t* tab = GTAB ? a.gtab + (uint64_t)blockIdx.x * 4096 : ltab;
     const uint32_t lane = threadIdx.x;
     const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
     for (uint64_t c = blockIdx.x; c < n_items; c += gridDim.x) {
@@ -453,6 +457,8 @@ struct sdfs_cdc_lz4 {
     int mode = SDFS_CDC_LZ4_R123;
     int num_cus = 256;
     int wg_per_cu = kLz4WgPerCu;  // SDFS_LZ4_WG_PER_CU overrides (measurements)
+    int gtab_mode = 0;            // SDFS_LZ4_GTAB=1: hash tables in global memory
+    ZBuf<uint32_t> gtab;
     hipStream_t stream = nullptr;
     ZBuf<uint64_t> bsum;
     // host-path scratch
@@ -475,10 +481,19 @@ namespace {
 int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
     if (a.n_max == 0) return SDFS_CDC_OK;
     const uint64_t grid = std::min<uint64_t>(a.n_max, (uint64_t)z->num_cus * z->wg_per_cu);
-    if (z->mode == SDFS_CDC_LZ4_V19)
+    if (z->gtab_mode) {
+        LZ_TRY(z->gtab.ensure(grid * 4096));
+        Lz4Args g = a;
+        g.gtab = z->gtab.p;
+        if (z->mode == SDFS_CDC_LZ4_V19)
+            hipLaunchKernelGGL((lz4_compress_kernel<SDFS_CDC_LZ4_V19, true>), dim3((uint32_t)grid), dim3(64), 0, s, g);
+        else
+            hipLaunchKernelGGL((lz4_compress_kernel<SDFS_CDC_LZ4_R123, true>), dim3((uint32_t)grid), dim3(64), 0, s, g);
+    } else if (z->mode == SDFS_CDC_LZ4_V19) {
         hipLaunchKernelGGL(lz4_compress_kernel<SDFS_CDC_LZ4_V19>, dim3((uint32_t)grid), dim3(64), 0, s, a);
-    else
+    } else {
         hipLaunchKernelGGL(lz4_compress_kernel<SDFS_CDC_LZ4_R123>, dim3((uint32_t)grid), dim3(64), 0, s, a);
+    }
     LZ_TRY(hipGetLastError());
     return SDFS_CDC_OK;
 }
@@ -506,6 +521,8 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     z->device = device;
     z->mode = mode;
     z->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (const char* v = getenv("SDFS_LZ4_GTAB")) z->gtab_mode = atoi(v);
+    if (z->gtab_mode) z->wg_per_cu = 24;
     if (const char* v = getenv("SDFS_LZ4_WG_PER_CU")) z->wg_per_cu = std::max(1, atoi(v));
     if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
         delete z;
@@ -522,6 +539,7 @@ int sdfs_cdc_lz4_destroy(sdfs_cdc_lz4* z) {
         (void)hipSetDevice(z->device);
         if (z->stream) (void)hipStreamSynchronize(z->stream);
         z->bsum.release();
+        z->gtab.release();
         z->h_in.release();
         z->h_out.release();
         z->h_soff.release();
