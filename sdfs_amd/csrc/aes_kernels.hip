@@ -103,36 +103,19 @@ struct Tab {
     // table word indexed by byte K (0 = least significant) of s
     template <int K>
     __device__ __forceinline__ uint32_t get(uint32_t s) const {
-        if constexpr (COPIES == 64 || COPIES == 16)
+        if constexpr (COPIES == 64)
             return at(__builtin_amdgcn_perm(s, l4, 0x0C0C0000u | ((4u + K) << 8)));
         else
             return at((((s >> (8 * K)) & 255u) << 7) | l4);
-    }
-    // COPIES == 16: the four rotated tables Te0..Te3 side by side, 16 copies each: word (x, t, c)
-    // at byte (x << 8) | (t << 6) | (c << 2), lane l reads copy l & 15 (2-way bank conflicts, no
-    // rotates; one v_perm per lookup).
-    template <int K, int TBL>
-    __device__ __forceinline__ uint32_t get4(uint32_t s) const {
-        return at(__builtin_amdgcn_perm(s, l4 | (TBL << 6), 0x0C0C0000u | ((4u + K) << 8)));
     }
 };
 
 template <int COPIES>
 __device__ __forceinline__ void fill_table(uint32_t* lds, const uint32_t* g, uint32_t nthreads) {
-    if constexpr (COPIES == 16) {  // x = i >> 6, table t = (i >> 4) & 3 holds ror(Te0[x], 8t)
-        for (uint32_t i = threadIdx.x; i < 256u * 64u; i += nthreads) {
-            const uint32_t v = g[i >> 6], t = (i >> 4) & 3;
-            lds[i] = t ? __builtin_amdgcn_alignbit(v, v, 8 * t) : v;
-        }
-    } else {
-        for (uint32_t i = threadIdx.x; i < 256u * COPIES; i += nthreads) lds[i] = g[i / COPIES];
-    }
+    for (uint32_t i = threadIdx.x; i < 256u * COPIES; i += nthreads) lds[i] = g[i / COPIES];
 }
 
-template <int COPIES>
-constexpr uint32_t tab_words() {
-    return COPIES == 16 ? 256u * 64u : 256u * COPIES;
-}
+
 
 template <int COPIES>
 __device__ __forceinline__ uint32_t lane_off() {
@@ -366,12 +349,8 @@ __device__ __forceinline__ uint32_t aes_encrypt_quad(uint32_t s, const Tab<COPIE
 #pragma unroll
     for (int r = 1; r < NR; r++) {
         const uint32_t s1 = quad_mov<kQuadNext1>(s), s2 = quad_mov<kQuadNext2>(s), s3 = quad_mov<kQuadNext3>(s);
-        if constexpr (COPIES == 16)
-            s = xor3(xor3(T.template get4<3, 0>(s), T.template get4<2, 1>(s1), T.template get4<1, 2>(s2)),
-                     T.template get4<0, 3>(s3), k[r]);
-        else
-            s = xor3(xor3(T.template get<3>(s), ror(T.template get<2>(s1), 8), ror(T.template get<1>(s2), 16)),
-                     ror(T.template get<0>(s3), 24), k[r]);
+        s = xor3(xor3(T.template get<3>(s), ror(T.template get<2>(s1), 8), ror(T.template get<1>(s2), 16)),
+                 ror(T.template get<0>(s3), 24), k[r]);
     }
     const uint32_t s1 = quad_mov<kQuadNext1>(s), s2 = quad_mov<kQuadNext2>(s), s3 = quad_mov<kQuadNext3>(s);
     return xor3(xor3((T.template get<3>(s) << 8) & 0xFF000000u, T.template get<2>(s1) & 0x00FF0000u,
@@ -409,7 +388,7 @@ __device__ __forceinline__ uint32_t load_be32(const uint8_t* p) {
 // (which set the kernel's floor) are not slowed by the short-record waves sharing their SIMD.
 template <int NR, int COPIES, int THREADS, bool PRIO = false>
 __global__ __launch_bounds__(THREADS) void aes_cbc_encrypt_quad_kernel(AesEncArgs a) {
-    __shared__ uint32_t lte[tab_words<COPIES>()];
+    __shared__ uint32_t lte[256 * COPIES];
     fill_table<COPIES>(lte, a.te0, THREADS);
     __syncthreads();
     const Tab<COPIES> T{lte, lane_off<COPIES>()};
@@ -645,34 +624,20 @@ void launch_enc_quad(uint64_t n_max, const AesEncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((aes_cbc_encrypt_quad_kernel<NR, COPIES, THREADS, PRIO>), dim3(g), dim3(THREADS), 0, s, a);
 }
 
-// variant 0: 32 table copies (32 KiB), 256-thread workgroups (5 per CU); 1: 64 copies with the
-// one-v_perm index (64 KiB), 512 threads (2 per CU); 2: 64 copies, 256 threads; 3/4: the quad
-// form (4 lanes per record) with 64 / 32 copies, 256 threads; 5: quad, 64 copies, 1024 threads;
-// 6 / 7: variants 4 / 3 with issue priority for waves of long records; 8: quad + priority with
-// the four rotated tables (no v_alignbit, 2-way bank conflicts); 9: quad + priority, 64 copies,
-// 512 threads.
+// variant 0: one lane per record, 32 table copies (32 KiB), 256-thread workgroups (5 per CU);
+// 3: the quad form (4 lanes per record), 64 copies with the one-v_perm index; 6: quad, 32 copies,
+// issue priority; 7 (production): quad, 64 copies, priority.  Measured and dropped (DESIGN.md
+// §13): 64 copies per lane (256 / 512 threads), quad with 512 / 1024 threads, four rotated tables.
 template <int NR>
 void launch_encrypt_nr(int variant, uint64_t n_max, const AesEncArgs& a, hipStream_t s) {
-    if (variant == 3)
+    if (variant == 0)
+        launch_enc<NR, 32, 256>(n_max, a, s);
+    else if (variant == 3)
         launch_enc_quad<NR, 64, 256>(n_max, a, s);
-    else if (variant == 5)
-        launch_enc_quad<NR, 64, 1024>(n_max, a, s);
     else if (variant == 6)
         launch_enc_quad<NR, 32, 256, true>(n_max, a, s);
-    else if (variant == 7)
-        launch_enc_quad<NR, 64, 256, true>(n_max, a, s);
-    else if (variant == 8)
-        launch_enc_quad<NR, 16, 256, true>(n_max, a, s);
-    else if (variant == 9)
-        launch_enc_quad<NR, 64, 512, true>(n_max, a, s);
-    else if (variant == 4)
-        launch_enc_quad<NR, 32, 256>(n_max, a, s);
-    else if (variant == 1)
-        launch_enc<NR, 64, 512>(n_max, a, s);
-    else if (variant == 2)
-        launch_enc<NR, 64, 256>(n_max, a, s);
     else
-        launch_enc<NR, 32, 256>(n_max, a, s);
+        launch_enc_quad<NR, 64, 256, true>(n_max, a, s);
 }
 
 void launch_encrypt(int nr, int variant, uint64_t n_max, const AesEncArgs& a, hipStream_t s) {

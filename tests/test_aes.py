@@ -276,7 +276,7 @@ def test_gpu_lz4_then_aes_chain():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [0, 3, 6, 7])
 def test_gpu_encrypt_variants_agree(variant, monkeypatch):
     """Every kernel layout (table copies, lane-per-record or quad-per-record) gives the oracle's bytes."""
     from sdfs_amd.aes import HipEncryptUtils
