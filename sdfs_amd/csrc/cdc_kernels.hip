@@ -1349,8 +1349,10 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
 // chain of ~1.4 k VALU instructions per 64-byte block (~2 us per block at full issue rate), so
 // the longest chunk of a batch (up to 2049 blocks with the backup profile's 128 KiB maxLen)
 // sets a floor under the kernel unless its wave is not slowed by the waves sharing its SIMD.
-template <int ALGO, int ABL = 0, int BS = 256, bool PF = false, bool PRIO = false>
-__global__ __launch_bounds__(BS) void chunk_hash_kernel(HashArgs a) {
+// WPE: minimum waves per SIMD the register allocation must allow (0 = compiler's choice).
+template <int ALGO, int ABL = 0, int BS = 256, bool PF = false, bool PRIO = false, int WPE = 0>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1, 8)))
+void chunk_hash_kernel(HashArgs a) {
     const uint32_t i = blockIdx.x * BS + threadIdx.x;
     if (i >= *a.total) return;
     if constexpr (PRIO) {
@@ -1403,6 +1405,10 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
             break;
         case 8: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         case 9: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, false>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 11: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 12: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true, 6>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 13: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 14: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true>), dim3(blocks), dim3(256), 0, s, a); break;
         case 10: hipLaunchKernelGGL((chunk_hash_kernel<0, 4, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;
         }
