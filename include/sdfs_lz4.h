@@ -70,6 +70,20 @@ int sdfs_cdc_lz4_compress(sdfs_cdc_lz4* z, const uint8_t* src, uint32_t n, uint8
 int sdfs_cdc_lz4_compress_batch(sdfs_cdc_lz4* z, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
                                 uint32_t n, uint8_t* out, const uint64_t* out_offs, uint32_t* out_lens, int framed);
 
+/* Read side (HashBlobArchive.getChunk -> CompressionUtils.decompressLz4(block, nz) =
+ * LZ4FastDecompressor.decompress, HashBlobArchive.java:1927-1933, CompressionUtils.java:122-125).
+ * Device batch: record i = d_src[d_src_off[i] .. + d_src_len[i]) decoded to d_out + d_dst_off[i]
+ * (room d_dst_cap[i]); d_dst_len[i] = decoded length, or UINT32_MAX for a malformed block.
+ * framed != 0: records are putChunk records [BE32 nz][payload]: nz > 0 = an LZ4 block that must
+ * decode to exactly nz bytes, else the payload is the raw chunk (copied). */
+int sdfs_cdc_lz4_decompress_device(sdfs_cdc_lz4* z, const uint8_t* d_src, const uint64_t* d_src_off,
+                                   const uint32_t* d_src_len, const uint32_t* d_count, uint64_t n_max, uint8_t* d_out,
+                                   const uint64_t* d_dst_off, const uint32_t* d_dst_cap, uint32_t* d_dst_len,
+                                   int framed, void* stream);
+/* LZ4FastDecompressor.decompress(src, destLen) on host bytes: SDFS_CDC_EINVAL unless the block
+ * decodes to exactly dst_len bytes. */
+int sdfs_cdc_lz4_decompress(sdfs_cdc_lz4* z, const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t dst_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,12 +95,24 @@ def main():
             for i in rng.integers(0, n, 32):
                 chunk = host[int(so[i]): int(so[i]) + int(sl[i])]
                 assert ob[int(do[i]): int(do[i]) + int(dl[i])].tobytes() == Z.compress_framed(chunk, mode), i
-            pending.append((ds, mname, mode, n, nbytes, ms, clen, so, sl))
+            # read side: decode the framed records back on the GPU (round trip checked)
+            back = torch.empty(nbytes + 16, dtype=torch.uint8, device="cuda")
+            blen = torch.empty(n, dtype=torch.int32, device="cuda")
+            comp.decompress_device(out, dst_off, dst_len, back, src_off, src_len, blen)
+            torch.cuda.synchronize()
+            ev[0].record(s)
+            for _ in range(REPS):
+                comp.decompress_device(out, dst_off, dst_len, back, src_off, src_len, blen)
+            ev[1].record(s)
+            torch.cuda.synchronize()
+            dms = ev[0].elapsed_time(ev[1]) / REPS
+            assert torch.equal(blen, src_len) and torch.equal(back[:nbytes], batch.data[:nbytes])
+            pending.append((ds, mname, mode, n, nbytes, ms, clen, so, sl, dms))
             comp.destroy()
     eng.destroy()
     # CPU oracle (C, THREADS pthreads) on a bounded sample of the same chunks -- after every GPU
     # measurement: a 16-thread CPU phase between two GPU timings halves the second one on the box
-    for ds, mname, mode, n, nbytes, ms, clen, so, sl in pending:
+    for ds, mname, mode, n, nbytes, ms, clen, so, sl, dms in pending:
         host = hosts[ds]
         rng = np.random.default_rng(2)
         order = rng.permutation(n)
@@ -116,6 +128,7 @@ def main():
             "bench": "lz4_unique_chunks", "data": ds, "mode": mname, "chunks": int(n),
             "input_gib": round(nbytes / 2**30, 3), "kernel_ms": round(ms, 3),
             "gibps": round(nbytes / (ms / 1e3) / 2**30, 1), "ratio": round(nbytes / max(clen, 1), 3),
+            "decompress_ms": round(dms, 3), "decompress_gibps": round(nbytes / (dms / 1e3) / 2**30, 1),
             "cpu_baseline": {"gibps": round(done_bytes / cpu_secs / 2**30, 3), "threads": THREADS,
                              "sample_chunks": int(k), "kind": "port (oracle/lz4_ref.c)"},
         }), flush=True)

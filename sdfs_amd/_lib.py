@@ -116,6 +116,9 @@ SIGNATURES = {
     "sdfs_cdc_lz4_compress": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _u32p]),
     "sdfs_cdc_lz4_compress_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp,
                                                    ctypes.c_int]),
+    "sdfs_cdc_lz4_decompress_device": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, _vp,
+                                                      ctypes.c_int, _vp]),
+    "sdfs_cdc_lz4_decompress": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32]),
     # include/sdfs_meta.h
     "sdfs_cdc_map_slot_bytes": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "sdfs_cdc_map_emit": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, _P(DevOut), ctypes.c_uint32, _vp, _vp, _vp,

@@ -101,8 +101,10 @@ __device__ __forceinline__ uint32_t put_run(uint8_t* dst, uint32_t op, uint32_t 
     return op + nff + 1;
 }
 
-// n bytes src -> dst (disjoint), 16 bytes per lane per step, four steps in flight
-__device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
+// n bytes src -> dst (disjoint), 16 bytes per lane per step, four steps in flight.  SrcPtr: a
+// global or an LDS (address_space(3)) byte pointer.
+template <typename SrcPtr>
+__device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, SrcPtr __restrict__ src, uint32_t n,
                                            uint32_t lane) {
     const uint32_t nv = n >> 4;
     uint32_t k = lane;
@@ -329,6 +331,129 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(Lz4Args a) {
             }
             a.dst_len[c] = len + hdr;
         }
+    }
+}
+
+// ---- decompression (the read side: HashBlobArchive.getChunk -> CompressionUtils.decompressLz4,
+// HashBlobArchive.java:1927-1933, CompressionUtils.java:122-125; LZ4 block format).  One wave per
+// block: the token stream is parsed as wave-uniform scalar work, literal runs are copied 16 bytes
+// per lane, and a match is copied lane-parallel — an overlapping match (offset < length) as
+// dst[op + k] = dst[op - off + k % off], which only reads bytes written before the match.
+struct Lz4DecArgs {
+    const uint8_t* src;
+    const uint64_t* src_off;
+    const uint32_t* src_len;
+    const uint32_t* d_count;
+    uint64_t n_max;
+    uint8_t* out;
+    const uint64_t* dst_off;
+    const uint32_t* dst_cap;
+    uint32_t* dst_len;
+    uint32_t framed;
+};
+
+constexpr uint32_t kLz4Corrupt = 0xFFFFFFFFu;
+
+// Decode one block of n bytes into dst (cap bytes); returns the decoded length or kLz4Corrupt.
+typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+
+template <typename SrcPtr>
+__device__ uint32_t decompress_block(SrcPtr __restrict__ src, uint32_t n, uint8_t* dst, uint32_t cap,
+                                     uint32_t lane) {
+    uint32_t ip = 0, op = 0;
+    for (;;) {
+        if (ip >= n) return kLz4Corrupt;
+        const uint32_t token = src[ip++];
+        uint32_t lit = token >> 4;
+        if (lit == kRunMask) {
+            uint32_t b;
+            do {
+                if (ip >= n) return kLz4Corrupt;
+                b = src[ip++];
+                lit += b;
+            } while (b == 255);
+        }
+        if (ip + lit > n || op + lit > cap) return kLz4Corrupt;
+        copy_bytes(dst + op, src + ip, lit, lane);
+        ip += lit;
+        op += lit;
+        if (ip == n) return op;  // the last sequence carries literals only
+        if (ip + 2 > n) return kLz4Corrupt;
+        const uint32_t off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
+        ip += 2;
+        if (off == 0 || off > op) return kLz4Corrupt;
+        uint32_t ml = token & kMlMask;
+        if (ml == kMlMask) {
+            uint32_t b;
+            do {
+                if (ip >= n) return kLz4Corrupt;
+                b = src[ip++];
+                ml += b;
+            } while (b == 255);
+        }
+        ml += kMinMatch;
+        if (op + ml > cap) return kLz4Corrupt;
+        if (off >= ml) {
+            copy_bytes(dst + op, (const uint8_t*)(dst + op - off), ml, lane);  // disjoint: source ends before op
+        } else {
+            uint32_t kr = lane % off;  // k % off, stepped by 64 without a division per byte
+            const uint32_t sr = 64 % off;
+            for (uint32_t k = lane; k < ml; k += 64) {
+                dst[op + k] = dst[op - off + kr];
+                kr += sr;
+                if (kr >= off) kr -= off;
+            }
+        }
+        op += ml;
+    }
+}
+
+constexpr uint32_t kDecStage = 8192;  // compressed bytes staged in LDS per wave (larger blocks parse from global)
+constexpr int kDecWgPerCu = 16;
+
+// a block: staged through LDS when it fits (the token/length/offset parse and the literal reads
+// become LDS round trips), else parsed from global memory
+__device__ __forceinline__ uint32_t decode_any(const uint8_t* in, uint32_t n, uint8_t* o, uint32_t cap, uint8_t* stage,
+                                               uint32_t lane) {
+    if (n <= kDecStage) {
+        copy_bytes(stage, in, n, lane);
+        __builtin_amdgcn_s_waitcnt(0);  // staged bytes written before any lane parses them
+        return decompress_block((lds_cu8*)stage, n, o, cap, lane);
+    }
+    return decompress_block(in, n, o, cap, lane);
+}
+
+__global__ __launch_bounds__(64) void lz4_decompress_kernel(Lz4DecArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kDecStage];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
+    for (uint64_t c = blockIdx.x; c < n_items; c += gridDim.x) {
+        const uint8_t* in = a.src + a.src_off[c];
+        uint32_t n = a.src_len[c];
+        uint8_t* o = a.out + a.dst_off[c];
+        uint32_t cap = a.dst_cap[c];
+        uint32_t got;
+        if (a.framed) {  // [BE32 nz][payload]: nz > 0 = LZ4 block of nz bytes, else raw bytes
+            if (n < 4) {
+                got = kLz4Corrupt;
+            } else {
+                const int32_t nz = (int32_t)((uint32_t)in[0] << 24 | (uint32_t)in[1] << 16 | (uint32_t)in[2] << 8 | in[3]);
+                in += 4;
+                n -= 4;
+                if (nz > 0) {
+                    got = (uint32_t)nz <= cap ? decode_any(in, n, o, (uint32_t)nz, stage, lane) : kLz4Corrupt;
+                    if (got != (uint32_t)nz) got = kLz4Corrupt;
+                } else if (n <= cap) {
+                    copy_bytes(o, in, n, lane);
+                    got = n;
+                } else {
+                    got = kLz4Corrupt;
+                }
+            }
+        } else {
+            got = decode_any(in, n, o, cap, stage, lane);
+        }
+        if (lane == 0) a.dst_len[c] = got;
     }
 }
 
@@ -643,6 +768,51 @@ int sdfs_cdc_lz4_compress(sdfs_cdc_lz4* z, const uint8_t* src, uint32_t n, uint8
     const uint64_t off = 0, doff = 0;
     const uint8_t dummy = 0;
     return sdfs_cdc_lz4_compress_batch(z, n ? src : &dummy, &off, &n, 1, dst, &doff, out_len, 0);
+}
+
+int sdfs_cdc_lz4_decompress_device(sdfs_cdc_lz4* z, const uint8_t* d_src, const uint64_t* d_src_off,
+                                   const uint32_t* d_src_len, const uint32_t* d_count, uint64_t n_max, uint8_t* d_out,
+                                   const uint64_t* d_dst_off, const uint32_t* d_dst_cap, uint32_t* d_dst_len,
+                                   int framed, void* stream) {
+    if (!z) return fail_status(SDFS_CDC_EINVAL, "null compressor");
+    if (n_max == 0) return SDFS_CDC_OK;
+    if (!d_src || !d_src_off || !d_src_len || !d_out || !d_dst_off || !d_dst_cap || !d_dst_len)
+        return fail_status(SDFS_CDC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(z->mu);
+    LZ_TRY(hipSetDevice(z->device));
+    Lz4DecArgs a{d_src, d_src_off, d_src_len, d_count, n_max, d_out, d_dst_off, d_dst_cap, d_dst_len, framed ? 1u : 0u};
+    const uint64_t grid = std::min<uint64_t>(n_max, (uint64_t)z->num_cus * kDecWgPerCu);
+    hipLaunchKernelGGL(lz4_decompress_kernel, dim3((uint32_t)grid), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                       a);
+    LZ_TRY(hipGetLastError());
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_lz4_decompress(sdfs_cdc_lz4* z, const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t dst_len) {
+    if (!z || (n && !src) || (dst_len && !dst)) return fail_status(SDFS_CDC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(z->mu);
+    LZ_TRY(hipSetDevice(z->device));
+    hipStream_t s = z->stream;
+    LZ_TRY(z->h_in.ensure(n + 16));
+    LZ_TRY(z->h_out.ensure((uint64_t)dst_len + 16));
+    LZ_TRY(z->h_soff.ensure(2));
+    LZ_TRY(z->h_slen.ensure(3));
+    const uint64_t offs[2] = {0, 0};
+    const uint32_t lens[2] = {n, dst_len};
+    if (n) LZ_TRY(hipMemcpyAsync(z->h_in.p, src, n, hipMemcpyHostToDevice, s));
+    LZ_TRY(hipMemcpyAsync(z->h_soff.p, offs, sizeof(offs), hipMemcpyHostToDevice, s));
+    LZ_TRY(hipMemcpyAsync(z->h_slen.p, lens, sizeof(lens), hipMemcpyHostToDevice, s));
+    Lz4DecArgs a{z->h_in.p, z->h_soff.p, z->h_slen.p, nullptr, 1, z->h_out.p, z->h_soff.p + 1, z->h_slen.p + 1,
+                 z->h_slen.p + 2, 0};
+    hipLaunchKernelGGL(lz4_decompress_kernel, dim3(1), dim3(64), 0, s, a);
+    LZ_TRY(hipGetLastError());
+    uint32_t got = 0;
+    LZ_TRY(hipMemcpyAsync(&got, z->h_slen.p + 2, 4, hipMemcpyDeviceToHost, s));
+    LZ_TRY(hipStreamSynchronize(s));
+    if (got != dst_len) return fail_status(SDFS_CDC_EINVAL, "malformed LZ4 block (decoded %d of %u bytes)",
+                                           got == kLz4Corrupt ? -1 : (int)got, dst_len);
+    if (dst_len) LZ_TRY(hipMemcpy(dst, z->h_out.p, dst_len, hipMemcpyDeviceToHost));
+    return SDFS_CDC_OK;
 }
 
 }  // extern "C"

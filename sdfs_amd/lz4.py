@@ -93,6 +93,28 @@ class HipLz4Compressor:
             count.data_ptr() if count is not None else None, n, out.data_ptr(), dst_off.data_ptr(),
             dst_len.data_ptr(), int(framed), s))
 
+    def decompress(self, block, n: int) -> bytes:
+        """LZ4FastDecompressor.decompress(src, destLen): IOError (SdfsCdcError) on a malformed block."""
+        a = np.frombuffer(bytes(block), np.uint8) if not isinstance(block, np.ndarray) else np.ascontiguousarray(
+            block, np.uint8)
+        out = np.zeros(max(n, 1), np.uint8)
+        check(self._lib.sdfs_cdc_lz4_decompress(self._h, a.ctypes.data if len(a) else None, len(a), out.ctypes.data,
+                                                int(n)))
+        return out[:n].tobytes()
+
+    def decompress_device(self, data, src_off, src_len, out, dst_off, dst_cap, dst_len, count=None,
+                          framed: bool = True, stream=None) -> None:
+        """Device tensors: data u8 (blocks or putChunk records), src_off i64[n], src_len i32[n], out u8,
+        dst_off i64[n], dst_cap i32[n]; dst_len i32[n] receives the decoded length or -1 (malformed)."""
+        import torch
+
+        n = int(src_len.shape[0])
+        s = stream if stream is not None else torch.cuda.current_stream(data.device).cuda_stream
+        check(self._lib.sdfs_cdc_lz4_decompress_device(
+            self._h, data.data_ptr(), src_off.data_ptr(), src_len.data_ptr(),
+            count.data_ptr() if count is not None else None, n, out.data_ptr(), dst_off.data_ptr(),
+            dst_cap.data_ptr(), dst_len.data_ptr(), int(framed), s))
+
     def plan_records(self, records, sel=None, count=None, buffer_id_base: int = 0, uniform_len: int = 0,
                      buf_offs=None, framed: bool = True, stream=None):
         """Extents + output offsets of selected 48-byte fingerprint records (device tensors).
@@ -115,6 +137,14 @@ class HipLz4Compressor:
 
 
 _default = {}
+
+
+def decompressLz4(data, n: int, device: int = 0) -> bytes:
+    """CompressionUtils.decompressLz4(input, len) (CompressionUtils.java:122-125) on the GPU."""
+    key = (R123, device)
+    if key not in _default:
+        _default[key] = HipLz4Compressor(R123, device)
+    return _default[key].decompress(data, n)
 
 
 def compressLz4(data, mode: int = R123, device: int = 0) -> bytes:

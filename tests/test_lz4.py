@@ -195,3 +195,55 @@ def test_gpu_device_path_new_chunks_from_the_index():
             assert rec == Z.compress_framed(chunk, mode), i
     ix.destroy()
     e.destroy()
+
+
+@pytest.mark.gpu
+def test_gpu_decompress_single_and_malformed():
+    """Read side: the GPU decoder restores every oracle block (both modes, all kinds/lengths)."""
+    c = comp(Z.R123)
+    for kind in KINDS:
+        for n in LENS:
+            d = _gen(kind, n, stream=5)
+            for mode in (Z.R123, Z.V19):
+                assert c.decompress(Z.compress(d, mode), n) == d, (kind, n, mode)
+    blk = bytearray(Z.compress(_gen("text", 5000, 9)))
+    with pytest.raises(_lib.SdfsCdcError):
+        c.decompress(bytes(blk), 4999)  # wrong length
+    bad = bytearray(blk)
+    bad[-3] = 0xF0  # a literal run past the end of the block
+    with pytest.raises(_lib.SdfsCdcError):
+        c.decompress(bytes(bad[:-1]), 5000)
+
+
+@pytest.mark.gpu
+def test_gpu_decompress_device_framed_records():
+    """putChunk records ([BE32 nz][LZ4 block], or nz = -1 with the raw chunk) decoded on the device."""
+    import struct
+
+    import torch
+
+    rng = np.random.default_rng(44)
+    recs, datas = [], []
+    for i in range(400):
+        kind = KINDS[i % len(KINDS)]
+        n = int(rng.integers(0, 40000))
+        d = _gen(kind, n, stream=300 + i)
+        datas.append(d)
+        recs.append(struct.pack(">i", -1) + d if i % 11 == 0 else Z.compress_framed(d))
+    src_off = np.concatenate([[0], np.cumsum([len(r) + 1 for r in recs[:-1]])]).astype(np.int64)
+    base = np.zeros(int(src_off[-1]) + len(recs[-1]) + 16, np.uint8)
+    for o, r in zip(src_off, recs):
+        base[int(o): int(o) + len(r)] = np.frombuffer(r, np.uint8)
+    caps = np.array([len(d) for d in datas], np.int32)
+    dst_off = np.concatenate([[3], 3 + np.cumsum(caps[:-1].astype(np.int64) + 5)]).astype(np.int64)
+    dev = torch.device("cuda:0")
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
+    out = torch.zeros(int(dst_off[-1] + caps[-1] + 16), dtype=torch.uint8, device=dev)
+    dl = torch.zeros(len(recs), dtype=torch.int32, device=dev)
+    comp(Z.R123).decompress_device(t(base, torch.uint8), t(src_off, torch.int64),
+                                   t([len(r) for r in recs], torch.int32), out, t(dst_off, torch.int64),
+                                   t(caps, torch.int32), dl, framed=True)
+    torch.cuda.synchronize()
+    o, dln = out.cpu().numpy(), dl.cpu().numpy()
+    for i, d in enumerate(datas):
+        assert dln[i] == len(d) and o[dst_off[i]: dst_off[i] + len(d)].tobytes() == d, i
