@@ -181,7 +181,7 @@ def main():
         eng2.destroy()
 
     # end-to-end (pinned host staging + H2D + kernels + D2H), rank 0 only
-    e2e = None
+    e2e = e2e_pinned = None
     if rank == 0 and args.e2e_mib > 0:
         nb = min(nbuf, args.e2e_mib * 1024 // args.buf_kib)
         host = batch.data[: nb * buf_len].cpu().numpy()
@@ -195,6 +195,17 @@ def main():
         for _ in range(reps):
             eng.chunk_batch(host, offs, lens)
         e2e = nb * buf_len * reps / (time.perf_counter() - te) / 2**30
+        # the same from pinned host memory (a JNI direct buffer registered with the driver): the
+        # engine copies to the GPU straight from it, no staging copy
+        hp = torch.empty(nb * buf_len, dtype=torch.uint8, pin_memory=True)
+        hp.copy_(batch.data[: nb * buf_len])
+        hpn = hp.numpy()
+        eng.chunk_batch(hpn, offs, lens)
+        te = time.perf_counter()
+        for _ in range(reps):
+            eng.chunk_batch(hpn, offs, lens)
+        e2e_pinned = nb * buf_len * reps / (time.perf_counter() - te) / 2**30
+        del hp, hpn
 
     if rank != 0:
         if use_ex:
@@ -253,6 +264,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "e2e_host_gibps": round(e2e, 3) if e2e else None,
+        "e2e_pinned_host_gibps": round(e2e_pinned, 3) if e2e_pinned else None,
         "pipelined_2stream": pipelined,
     }
     print(json.dumps(res), flush=True)

@@ -63,7 +63,7 @@ typedef struct sdfs_cdc_params {
     uint32_t hash_algo;     /* enum sdfs_cdc_hash_algo */
     int32_t device;         /* HIP device ordinal */
     uint32_t flags;         /* reserved, 0 */
-    uint64_t max_batch_bytes; /* host-batch staging size (pinned); 0 = default 256 MiB */
+    uint64_t max_batch_bytes; /* host-batch staging per slot (pinned, two slots); 0 = default 256 MiB */
 } sdfs_cdc_params;
 
 typedef struct sdfs_cdc_engine sdfs_cdc_engine;

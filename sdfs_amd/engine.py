@@ -75,6 +75,7 @@ class SdfsConfig:
     pred_mask: int = 0xFFF
     pred_value: int = 0
     min_cmp: int = MIN_GT
+    max_batch_bytes: int = 0  # host-batch pinned staging per slot (0 = the engine default, 256 MiB)
 
     @classmethod
     def backup_volume(cls, **kw) -> "SdfsConfig":
@@ -130,6 +131,7 @@ class SdfsConfig:
         p.pred_mask = self.pred_mask
         p.pred_value = self.pred_value
         p.min_cmp = self.min_cmp
+        p.max_batch_bytes = self.max_batch_bytes
         ht = (hash_type or self.hash_type).upper()
         if ht not in _ALGO:
             raise ValueError(f"hash-type {ht} has no variable engine (HashFunctionPool.java:102-121)")

@@ -377,3 +377,23 @@ def test_get_hash_batch_and_device_extents(algo):
         assert out[i, :dl].tobytes() == hf(chunks[i])[:dl], i
     assert not out[k:].any()
     e.destroy()
+
+
+@pytest.mark.gpu
+def test_pinned_host_batch_direct_copy_matches_pageable():
+    """Pinned caller memory takes the no-staging H2D path; results equal the pageable path's."""
+    import torch
+
+    e = HipVariableSha256HashEngine()
+    nb, L = 96, 262144
+    data = np.concatenate([O.synth(SYNTH_SEED, 900 + i, 0, L) for i in range(nb)])
+    pin = torch.empty(nb * L, dtype=torch.uint8, pin_memory=True)
+    pin.copy_(torch.from_numpy(data))
+    offs = np.arange(nb, dtype=np.uint64) * L
+    for lens in (np.full(nb, L, np.uint32),  # back to back, 64-byte multiples: direct copy
+                 np.array([L - (i % 7) * 13 for i in range(nb)], np.uint32)):  # ragged: staged
+        a = e.chunk_batch(data, offs, lens)
+        b = e.chunk_batch(pin.numpy(), offs, lens)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    e.destroy()
