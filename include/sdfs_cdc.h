@@ -112,6 +112,12 @@ uint32_t sdfs_cdc_slot_cap(const sdfs_cdc_engine* e, uint64_t buf_len);
  * Host bytes in, digest_len bytes out (computed on the GPU). */
 int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest);
 
+/* Page-lock caller memory (e.g. the flush buffers a JNI shim allocates as direct ByteBuffers) so
+ * sdfs_cdc_get_chunks_batch copies it to the GPU in place instead of through its staging slots
+ * (hipHostRegister / hipHostUnregister). */
+int sdfs_cdc_host_register(void* p, uint64_t n);
+int sdfs_cdc_host_unregister(void* p);
+
 /* ---- getHash in bulk: many chunks fingerprinted in one GPU pass ----
  * The getHash callers that verify or key whole chunks (HashBlobArchive.java:1271-1276 VERIFY_WRITES,
  * :1936-1940 VERIFY_READS; HashStore.java:63-71; WritableCacheBuffer.java:93-97) one call per chunk

@@ -95,6 +95,8 @@ SIGNATURES = {
     "sdfs_cdc_kernel_times": (ctypes.c_int, [_vp, _P(ctypes.c_char_p), _P(ctypes.c_float), ctypes.c_int]),
     "sdfs_cdc_synth_device": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                              ctypes.c_uint64, _vp]),
+    "sdfs_cdc_host_register": (ctypes.c_int, [_vp, ctypes.c_uint64]),
+    "sdfs_cdc_host_unregister": (ctypes.c_int, [_vp]),
     "sdfs_cdc_get_hash_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "sdfs_cdc_hash_device": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     # include/sdfs_index.h

@@ -1024,6 +1024,18 @@ int hash_extents(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_of
 }
 }  // namespace
 
+int sdfs_cdc_host_register(void* p, uint64_t n) {
+    if (!p || !n) return fail(SDFS_CDC_EINVAL, "null or empty region");
+    HIP_TRY(hipHostRegister(p, n, hipHostRegisterDefault));
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_host_unregister(void* p) {
+    if (!p) return fail(SDFS_CDC_EINVAL, "null region");
+    HIP_TRY(hipHostUnregister(p));
+    return SDFS_CDC_OK;
+}
+
 int sdfs_cdc_hash_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
                          const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, void* stream) {
     if (!e) return fail(SDFS_CDC_EINVAL, "null engine");

@@ -396,4 +396,14 @@ def test_pinned_host_batch_direct_copy_matches_pageable():
         b = e.chunk_batch(pin.numpy(), offs, lens)
         for x, y in zip(a, b):
             assert np.array_equal(x, y)
+    # caller memory page-locked through the C-ABI (what a JNI shim does with its direct buffers)
+    reg = np.array(data)  # a fresh, page-aligned-enough numpy buffer
+    _lib.check(_lib.load().sdfs_cdc_host_register(reg.ctypes.data, reg.nbytes))
+    try:
+        c = e.chunk_batch(reg, offs, np.full(nb, L, np.uint32))
+        a = e.chunk_batch(data, offs, np.full(nb, L, np.uint32))
+        for x, y in zip(a, c):
+            assert np.array_equal(x, y)
+    finally:
+        _lib.check(_lib.load().sdfs_cdc_host_unregister(reg.ctypes.data))
     e.destroy()
