@@ -142,3 +142,68 @@ class RecordExchange:
         mx = max(counts) if counts else 0
         return torch.cat([gathered[r * mx: r * mx + c] for r, c in enumerate(counts)], 0) if mx else \
             gathered.new_empty((0, RECORD_BYTES))
+
+
+# ---- partitioned dedup-hit index across ranks (SURVEY.md 8(e) "alternative") ----------------
+
+def shard_of(records: torch.Tensor, world: int, hash_len: int = 32) -> torch.Tensor:
+    """Owner rank of each record's fingerprint: RocksDBMap's shard rule generalised to `world`
+    shards (RocksDBMap.java:373-379 with dbs.length = 8: l = key[last] as a signed byte, l < 0 ->
+    -l + 127, shard = l / 32); here shard = l * world / 256, identical to it at world = 8."""
+    last = records[:, hash_len - 1].to(torch.int64)
+    l = torch.where(last >= 128, (256 - last) + 127, last)  # signed byte b < 0 -> -b + 127
+    return (l * world) // 256
+
+
+class ShardedDedupIndex:
+    """The dedup-hit index split across ranks by fingerprint: every rank owns one shard (its
+    ``index``: a HipHashesMap, or any object with the same ``put_records``).
+
+    ``put_records(table, count)`` — this rank's fingerprint records (e.g. its engine's record
+    table) — routes every record to its owner with one all-to-all, applies them there in
+    (source rank, record) order, and returns each record's ``(dup u8[n], hashloc int64[n])`` to
+    its writer with a second all-to-all, in the caller's record order.  A fingerprint first
+    written by several ranks in the same batch is inserted once: the lowest rank's copy wins and
+    the others get ``dup = 1`` and its position.  Positions are ``pos_base + (rank << 40) + k``.
+    """
+
+    def __init__(self, index, group=None, hash_len: int = 32):
+        self.index = index
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.hash_len = hash_len
+
+    def put_records(self, table: torch.Tensor, count, pos_base: int = 0):
+        dev = table.device
+        n = int(count.item()) if isinstance(count, torch.Tensor) else int(count)
+        recs = table[:n]
+        owner = shard_of(recs, self.world, self.hash_len) if n else torch.zeros(0, dtype=torch.int64, device=dev)
+        order = torch.argsort(owner, stable=True)
+        send = recs[order].contiguous()
+        send_counts = torch.bincount(owner, minlength=self.world).to(torch.int64)
+        recv_counts = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        sc, rc = send_counts.tolist(), recv_counts.tolist()
+        recv = torch.empty(sum(rc), RECORD_BYTES, dtype=torch.uint8, device=dev)
+        dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc, group=self.group)
+        # apply in (source rank, record) order on this rank's shard
+        m = recv.shape[0]
+        if m:
+            dup, loc, _, _ = self.index.put_records(recv, None, pos_base=pos_base + (self.rank << 40))
+            dup, loc = dup[:m], loc[:m]
+        else:
+            dup = torch.zeros(0, dtype=torch.uint8, device=dev)
+            loc = torch.zeros(0, dtype=torch.int64, device=dev)
+        # results back to the writers, then into the caller's record order
+        back_dup = torch.empty(n, dtype=torch.uint8, device=dev)
+        back_loc = torch.empty(n, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(back_dup, dup.contiguous(), output_split_sizes=sc, input_split_sizes=rc,
+                               group=self.group)
+        dist.all_to_all_single(back_loc, loc.contiguous(), output_split_sizes=sc, input_split_sizes=rc,
+                               group=self.group)
+        out_dup = torch.empty_like(back_dup)
+        out_loc = torch.empty_like(back_loc)
+        out_dup[order] = back_dup
+        out_loc[order] = back_loc
+        return out_dup, out_loc

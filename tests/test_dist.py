@@ -109,3 +109,87 @@ def test_shard_streams_partition():
         parts = [shard_streams(n, w, r) for r in range(w)]
         flat = [s for p in parts for s in p]
         assert flat == list(range(n))
+
+
+class _DictIndex:
+    """CPU stand-in with HipHashesMap.put_records semantics (first copy in record order inserted at
+    pos_base + its insertion rank, later copies dup with that position) for the gloo test."""
+
+    def __init__(self):
+        self.pos = {}
+
+    def put_records(self, recs, count, pos_base=0):
+        n = recs.shape[0]
+        dup = torch.zeros(n, dtype=torch.uint8)
+        loc = torch.zeros(n, dtype=torch.int64)
+        for i in range(n):
+            key = bytes(recs[i, :32].tolist())
+            if key in self.pos:
+                dup[i], loc[i] = 1, self.pos[key]
+            else:
+                self.pos[key] = pos_base + len(self.pos)
+                loc[i] = self.pos[key]
+        return dup, loc, None, None
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sdfs_amd.dist import ShardedDedupIndex
+        g = torch.Generator().manual_seed(7)
+        pool = torch.randint(0, 256, (40, 32), generator=g, dtype=torch.uint8)  # shared fingerprints
+        rg = torch.Generator().manual_seed(100 + rank)
+        picks = torch.randint(0, 40, (25 + 5 * rank,), generator=rg)
+        table = torch.zeros(40, RECORD_BYTES, dtype=torch.uint8)
+        n = picks.shape[0]
+        table[:n, :32] = pool[picks]
+        table[:n, 32] = rank
+        table[:n, 33] = torch.arange(n, dtype=torch.uint8)
+        idx = ShardedDedupIndex(_DictIndex(), hash_len=32)
+        dup, loc = idx.put_records(table, torch.tensor([n]))
+        dup2, loc2 = idx.put_records(table, torch.tensor([n]))  # everything is known now
+        q.put((rank, picks.tolist(), dup.tolist(), loc.tolist(), dup2.tolist(), loc2.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_dedup_index_gloo(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    # reference: one global serial pass in (rank, record) order decides the first writer
+    first = {}
+    for r in range(world):
+        for i, f in enumerate(res[r][0]):
+            first.setdefault(f, (r, i))
+    pos_of = {}
+    for r in range(world):
+        picks, dup, loc, dup2, loc2 = res[r]
+        for i, f in enumerate(picks):
+            assert dup[i] == (0 if first[f] == (r, i) else 1), (r, i)
+            pos_of.setdefault(f, set()).add(loc[i])
+            assert dup2[i] == 1 and loc2[i] == loc[i]
+    assert all(len(v) == 1 for v in pos_of.values())  # one position per fingerprint, everywhere
+    assert len({next(iter(v)) for v in pos_of.values()}) == len(pos_of)
+
+
+def test_shard_of_matches_rocksdb_rule():
+    from sdfs_amd.dist import shard_of
+    recs = torch.zeros(256, RECORD_BYTES, dtype=torch.uint8)
+    recs[:, 31] = torch.arange(256, dtype=torch.uint8)
+    got = shard_of(recs, 8).tolist()
+    for b in range(256):
+        l = b - 256 if b >= 128 else b  # Java signed byte
+        if l < 0:
+            l = (l * -1) + 127
+        assert got[b] == l // 32, b

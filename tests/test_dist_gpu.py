@@ -48,3 +48,38 @@ def test_record_exchange_rccl_world1_overlapped_steps():
         eng.destroy()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_dedup_index_rccl_world1_matches_local_index():
+    import torch
+    import torch.distributed as dist
+
+    from sdfs_amd import HipVariableSha256HashEngine
+    from sdfs_amd.device import DeviceBatch
+    from sdfs_amd.dist import ShardedDedupIndex
+    from sdfs_amd.index import HipHashesMap
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        eng = HipVariableSha256HashEngine()
+        batch = DeviceBatch(eng, nbuf=64, buf_len=262144)
+        batch.fill_streams(first_stream=3, bufs_per_stream=8)
+        v = batch.data.view(64, 262144)
+        v[32:].copy_(v[:32])  # half the buffers repeat: duplicates across the batch
+        batch.run()
+        recs = batch.record_table()
+        ref_ix, sh_ix = HipHashesMap(1 << 16), HipHashesMap(1 << 16)
+        dup_r, loc_r, _, _ = ref_ix.put_records(recs, None, pos_base=5)
+        dup_s, loc_s = ShardedDedupIndex(sh_ix).put_records(recs, batch.total, pos_base=5)
+        torch.cuda.synchronize()
+        n = recs.shape[0]
+        assert torch.equal(dup_s, dup_r[:n]) and torch.equal(loc_s, loc_r[:n])
+        assert int(dup_s.sum()) >= n // 2
+        ref_ix.destroy()
+        sh_ix.destroy()
+        eng.destroy()
+    finally:
+        dist.destroy_process_group()
