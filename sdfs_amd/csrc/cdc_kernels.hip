@@ -1148,6 +1148,9 @@ constexpr uint32_t kSha256K[64] = {
 
 // SHA-256 compression (FIPS 180-4 6.2.2) on 16 big-endian message words; rotations map to
 // v_alignbit_b32, the Sigma xors and Ch/Maj to v_bitop3_b32, the three-input sums to v_add3_u32.
+// SB (sweep builds): a scheduling barrier after every round, so hipcc cannot overlap rounds
+// (lower register pressure, less ILP).
+template <bool SB = false>
 __device__ __forceinline__ void sha256_compress(uint32_t (&s)[8], uint32_t (&w)[16]) {
     uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
 #pragma clang loop unroll(full)
@@ -1175,6 +1178,7 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&s)[8], uint32_t (&w)[
         const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
         const uint32_t mj = maj3(a, b, c);
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
     }
     s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
 }
@@ -1312,7 +1316,7 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
 #pragma unroll
             for (int j = 0; j < 16; j++) s[j & 7] ^= w[j];
         } else if constexpr (SHA) {
-            sha256_compress(s, w);
+            sha256_compress<(ABL & 8) != 0>(s, w);
         } else {
             uint32_t m4[4] = {s[0], s[1], s[2], s[3]};
             md5_compress(m4, w);
@@ -1409,6 +1413,8 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
         case 12: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true, 6>), dim3(blocks), dim3(256), 0, s, a); break;
         case 13: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
         case 14: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 15: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 16: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         case 10: hipLaunchKernelGGL((chunk_hash_kernel<0, 4, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;
         }
