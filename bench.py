@@ -72,6 +72,8 @@ def main():
                     help="min-variable-segment-size (minLen = KiB*1024-1; 4 = the reference default)")
     ap.add_argument("--mask-bits", type=int, default=12,
                     help="boundary predicate (fp & (2^bits-1)) == 0 (12 = the default knob, SURVEY.md A.3)")
+    ap.add_argument("--hash-type", default="VARIABLE_SHA256",
+                    choices=["VARIABLE_SHA256", "VARIABLE_SHA256_160", "VARIABLE_MD5"])
     ap.add_argument("--ramp-secs", type=float, default=0.3, help="untimed clock ramp before the warmup steps")
     ap.add_argument("--pipelined", type=int, default=1, help="also time two batches in flight (N = 1)")
     ap.add_argument("--exchange", type=int, default=-1,
@@ -94,13 +96,13 @@ def main():
             os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
-    from sdfs_amd import HipVariableSha256HashEngine, SdfsConfig
+    from sdfs_amd import HashFunctionPool, SdfsConfig
     from sdfs_amd.device import DeviceBatch
     from sdfs_amd.dist import RecordExchange, shard_streams
 
     cfg = SdfsConfig(chunk_length=args.buf_kib * 1024, min_len=args.min_seg_kib * 1024 - 1,
-                     pred_mask=(1 << args.mask_bits) - 1)
-    eng = HipVariableSha256HashEngine(config=cfg, device=local)
+                     pred_mask=(1 << args.mask_bits) - 1, hash_type=args.hash_type)
+    eng = HashFunctionPool(cfg, device=local).getHashEngine()
     buf_len = args.buf_kib * 1024
     bufs_per_stream = args.stream_mib * 1024 // args.buf_kib
     streams = shard_streams(args.streams * world, world, rank)
@@ -167,7 +169,7 @@ def main():
     # value (which stays the one-stream rate the roofline's launch durations describe).
     pipelined = None
     if world == 1 and args.pipelined:
-        eng2 = HipVariableSha256HashEngine(config=cfg, device=local)
+        eng2 = HashFunctionPool(cfg, device=local).getHashEngine()
         batch2 = DeviceBatch(eng2, nbuf=nbuf, buf_len=buf_len, device=f"cuda:{local}")
         batch2.data = batch.data
         ss = [cs, torch.cuda.Stream()]
@@ -249,7 +251,7 @@ def main():
             "workload": f"{args.streams} streams x {args.stream_mib} MiB per GPU, CHUNK_LENGTH {buf_len} B "
                         f"({nbuf} buffers, {nbytes / 2**30:.2f} GiB per GPU), fresh CDC state per buffer",
             "params": f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
-                      f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen SHA-256",
+                      f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen {args.hash_type}",
             "mean_chunk_bytes": round(nbytes / max(total, 1), 1),
             "chunks_per_gpu_step": total,
             "exchange": "RCCL all_gather of 48-B fingerprint records, pipelined" if use_ex else "none (N=1)",
