@@ -298,3 +298,49 @@ def test_gpu_encrypt_variants_agree(variant, monkeypatch):
         for d, out in zip(datas, outs):
             assert out == A.cbc_encrypt(key, iv, d, prefix=pre)
     c.destroy()
+
+
+@pytest.mark.gpu
+def test_gpu_store_record_round_trip_on_device():
+    """The stored-record chain both ways in HBM: chunk -> LZ4 putChunk record -> AES-CBC, then
+    AES-CBC decrypt -> record decode -> the original chunk bytes (HashBlobArchive.putChunk /
+    getChunk with compression and encryption on)."""
+    import torch
+
+    from sdfs_amd.lz4 import HipLz4Compressor
+
+    key, iv = _key(32, 11), bytes(range(16))
+    c = ciph(key)
+    z = HipLz4Compressor()
+    rng = np.random.default_rng(52)
+    n = 500
+    lens = rng.integers(0, 33000, n).astype(np.int64)
+    kinds = [Z.text_like, Z.mixed]
+    datas = [kinds[i % 2](3, i, int(L)) if L else np.zeros(0, np.uint8) for i, L in enumerate(lens)]
+    src_off = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    data = np.concatenate(datas) if lens.sum() else np.zeros(1, np.uint8)
+    dev = torch.device("cuda:0")
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
+    d_data, d_soff, d_slen = t(data, torch.uint8), t(src_off, torch.int64), t(lens, torch.int32)
+    zroom = lens + lens // 255 + 20
+    zoff = np.concatenate([[0], np.cumsum(zroom[:-1])]).astype(np.int64)
+    zout = torch.zeros(int(zroom.sum()), dtype=torch.uint8, device=dev)
+    zlen = torch.zeros(n, dtype=torch.int32, device=dev)
+    z.compress_device(d_data, d_soff, d_slen, zout, t(zoff, torch.int64), zlen, framed=True)
+    aroom = zroom + 16
+    aoff = np.concatenate([[0], np.cumsum(aroom[:-1])]).astype(np.int64)
+    aout = torch.zeros(int(aroom.sum()), dtype=torch.uint8, device=dev)
+    alen = torch.zeros(n, dtype=torch.int32, device=dev)
+    c.encrypt_device(zout, t(zoff, torch.int64), zlen, aout, t(aoff, torch.int64), alen, iv=iv)
+    # read side
+    plain = torch.zeros_like(zout)
+    plen = torch.zeros(n, dtype=torch.int32, device=dev)
+    c.decrypt_device(aout, t(aoff, torch.int64), alen, plain, t(zoff, torch.int64), plen, iv=iv)
+    back = torch.zeros(max(int(lens.sum()), 1) + 64, dtype=torch.uint8, device=dev)
+    blen = torch.zeros(n, dtype=torch.int32, device=dev)
+    z.decompress_device(plain, t(zoff, torch.int64), plen, back, d_soff, d_slen, blen, framed=True)
+    torch.cuda.synchronize()
+    assert torch.equal(plen, zlen)
+    assert torch.equal(blen, d_slen)
+    assert torch.equal(back[:int(lens.sum())], d_data[:int(lens.sum())])
+    z.destroy()
