@@ -55,21 +55,40 @@ struct Lz4Args {
 // LDS byte scratch accessed as volatile LDS (ds_write_b8 / ds_read_u8, ordered per wave): a
 // volatile GENERIC pointer would become flat accesses with system-scope bits and vmcnt(0) waits.
 typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
+typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
 
-__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+template <typename P>
+__device__ __forceinline__ uint32_t ld32(P p) {
     uint32_t v;
     __builtin_memcpy(&v, p, 4);
     return v;
 }
-__device__ __forceinline__ uint64_t ld64(const uint8_t* p) {
+template <typename P>
+__device__ __forceinline__ uint64_t ld64(P p) {
     uint64_t v;
     __builtin_memcpy(&v, p, 8);
     return v;
 }
 
+// LDS source (STAGE kernels): unaligned words from two aligned dword reads and a v_alignbyte (a
+// plain unaligned 4-byte read from LDS compiles to four ds_read_u8).  The stage has 16 spare bytes
+// so the dword after the chunk's last byte is still inside it.
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+__device__ __forceinline__ uint32_t ld32(lds_cu8* p) {
+    const uint32_t a = (uint32_t)(uintptr_t)p;
+    lds_cu32* q = (lds_cu32*)(p - (a & 3));
+    return __builtin_amdgcn_alignbyte(q[1], q[0], a & 3);
+}
+__device__ __forceinline__ uint64_t ld64(lds_cu8* p) {
+    const uint32_t a = (uint32_t)(uintptr_t)p;
+    lds_cu32* q = (lds_cu32*)(p - (a & 3));
+    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, a & 3) << 32 | __builtin_amdgcn_alignbyte(w1, w0, a & 3);
+}
+
 // table index of the sequence at p (lz4_ref.c hash_at)
-template <int MODE>
-__device__ __forceinline__ uint32_t lz4_hash(const uint8_t* p, bool u16) {
+template <int MODE, typename P>
+__device__ __forceinline__ uint32_t lz4_hash(P p, bool u16) {
     if (u16) return (ld32(p) * 2654435761u) >> 19;
     if constexpr (MODE == SDFS_CDC_LZ4_V19) return (uint32_t)(((ld64(p) << 24) * 889523592379ull) >> 52);
     return (ld32(p) * 2654435761u) >> 20;
@@ -127,8 +146,25 @@ __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, SrcPtr __r
     for (uint32_t b = (nv << 4) + lane; b < n; b += 64) dst[b] = src[b];
 }
 
+// LDS source: the byte offset within a dword is the same for every lane (16 B per lane), so each
+// lane reads five aligned dwords and realigns them
+__device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, lds_cu8* __restrict__ src, uint32_t n,
+                                           uint32_t lane) {
+    const uint32_t a = (uint32_t)(uintptr_t)src, sh = a & 3;
+    lds_cu32* q = (lds_cu32*)(src - sh);
+    const uint32_t nv = n >> 4;
+    for (uint32_t k = lane; k < nv; k += 64) {
+        const uint32_t w0 = q[4 * k], w1 = q[4 * k + 1], w2 = q[4 * k + 2], w3 = q[4 * k + 3], w4 = q[4 * k + 4];
+        const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                   __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+        __builtin_memcpy(dst + 16 * k, &v, 16);
+    }
+    for (uint32_t b = (nv << 4) + lane; b < n; b += 64) dst[b] = src[b];
+}
+
 // number of equal bytes src[a0+k] == src[b0+k] with a0+k < lim (LZ4_count), 256 per step
-__device__ __forceinline__ uint32_t match_count(const uint8_t* src, uint32_t a0, uint32_t b0, uint32_t lim,
+template <typename SrcPtr>
+__device__ __forceinline__ uint32_t match_count(SrcPtr src, uint32_t a0, uint32_t b0, uint32_t lim,
                                                 uint32_t lane) {
     if (a0 >= lim) return 0;
     const uint32_t total = lim - a0;
@@ -155,8 +191,8 @@ __device__ __forceinline__ uint32_t match_count(const uint8_t* src, uint32_t a0,
 }
 
 // One chunk, one wave (all lanes run the same scalar control flow).  Returns the block length.
-template <int MODE>
-__device__ uint32_t compress_chunk(const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ dst,
+template <int MODE, typename SrcPtr>
+__device__ uint32_t compress_chunk(SrcPtr __restrict__ src, uint32_t n, uint8_t* __restrict__ dst,
                                    uint32_t* tab, lds_vu8* scr, uint32_t lane) {
     {
         uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -310,18 +346,29 @@ __device__ uint32_t compress_chunk(const uint8_t* __restrict__ src, uint32_t n, 
 // hundreds of chunks per workgroup, and a shared counter would serialise ~10^6 dequeues).
 // GTAB: the hash table lives in global memory (L2 / Infinity Cache) instead of LDS, so LDS no
 // longer caps the chunks in flight per CU (1 KiB of LDS per wave instead of 17 KiB).
-template <int MODE, bool GTAB = false>
+template <int MODE, bool GTAB = false, int STAGE = 0>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(Lz4Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t ltab[GTAB ? 4 : 4096];
     __shared__ uint8_t scr[kScrBuckets];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE > 0 ? STAGE + 16 : 16];
     uint32_t* tab = GTAB ? a.gtab + (uint64_t)blockIdx.x * 4096 : ltab;
     const uint32_t lane = threadIdx.x;
     const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
     for (uint64_t c = blockIdx.x; c < n_items; c += gridDim.x) {
         const uint32_t n = a.src_len[c];
+        const uint8_t* src = a.data + a.src_off[c];
         uint8_t* o = a.out + a.dst_off[c];
         const uint32_t hdr = a.framed ? 4u : 0u;
-        const uint32_t len = compress_chunk<MODE>(a.data + a.src_off[c], n, o + hdr, tab, (lds_vu8*)scr, lane);
+        uint32_t len;
+        if (STAGE > 0 && n <= (uint32_t)STAGE) {
+            // STAGE: the chunk's bytes in LDS, so every probe, candidate, catch-up, extension and
+            // literal read is an LDS round trip instead of an L2 one
+            copy_bytes(stage, src, n, lane);
+            __builtin_amdgcn_s_waitcnt(0);  // staged bytes written before any lane reads them
+            len = compress_chunk<MODE>((lds_cu8*)stage, n, o + hdr, tab, (lds_vu8*)scr, lane);
+        } else {
+            len = compress_chunk<MODE>(src, n, o + hdr, tab, (lds_vu8*)scr, lane);
+        }
         if (lane == 0) {
             if (hdr) {
                 o[0] = (uint8_t)(n >> 24);
@@ -331,6 +378,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(Lz4Args a) {
             }
             a.dst_len[c] = len + hdr;
         }
+        if (STAGE > 0) __builtin_amdgcn_s_waitcnt(0);  // every lane's stage reads done before the next copy
     }
 }
 
@@ -355,7 +403,6 @@ struct Lz4DecArgs {
 constexpr uint32_t kLz4Corrupt = 0xFFFFFFFFu;
 
 // Decode one block of n bytes into dst (cap bytes); returns the decoded length or kLz4Corrupt.
-typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
 
 template <typename SrcPtr>
 __device__ uint32_t decompress_block(SrcPtr __restrict__ src, uint32_t n, uint8_t* dst, uint32_t cap,
@@ -424,7 +471,7 @@ __device__ __forceinline__ uint32_t decode_any(const uint8_t* in, uint32_t n, ui
 }
 
 __global__ __launch_bounds__(64) void lz4_decompress_kernel(Lz4DecArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kDecStage];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kDecStage + 16];  // + the realigning reads' spare dword
     const uint32_t lane = threadIdx.x;
     const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
     for (uint64_t c = blockIdx.x; c < n_items; c += gridDim.x) {
@@ -583,6 +630,7 @@ struct sdfs_cdc_lz4 {
     int num_cus = 256;
     int wg_per_cu = kLz4WgPerCu;  // SDFS_LZ4_WG_PER_CU overrides (measurements)
     int gtab_mode = 0;            // SDFS_LZ4_GTAB=1: hash tables in global memory
+    int stage = 0;                // SDFS_LZ4_STAGE=16384|32768: chunks up to that size staged in LDS
     ZBuf<uint32_t> gtab;
     hipStream_t stream = nullptr;
     ZBuf<uint64_t> bsum;
@@ -614,6 +662,16 @@ int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
             hipLaunchKernelGGL((lz4_compress_kernel<SDFS_CDC_LZ4_V19, true>), dim3((uint32_t)grid), dim3(64), 0, s, g);
         else
             hipLaunchKernelGGL((lz4_compress_kernel<SDFS_CDC_LZ4_R123, true>), dim3((uint32_t)grid), dim3(64), 0, s, g);
+    } else if (z->stage == 32768) {
+        if (z->mode == SDFS_CDC_LZ4_V19)
+            hipLaunchKernelGGL((lz4_compress_kernel<SDFS_CDC_LZ4_V19, false, 32768>), dim3((uint32_t)grid), dim3(64), 0, s, a);
+        else
+            hipLaunchKernelGGL((lz4_compress_kernel<SDFS_CDC_LZ4_R123, false, 32768>), dim3((uint32_t)grid), dim3(64), 0, s, a);
+    } else if (z->stage == 16384) {
+        if (z->mode == SDFS_CDC_LZ4_V19)
+            hipLaunchKernelGGL((lz4_compress_kernel<SDFS_CDC_LZ4_V19, false, 16384>), dim3((uint32_t)grid), dim3(64), 0, s, a);
+        else
+            hipLaunchKernelGGL((lz4_compress_kernel<SDFS_CDC_LZ4_R123, false, 16384>), dim3((uint32_t)grid), dim3(64), 0, s, a);
     } else if (z->mode == SDFS_CDC_LZ4_V19) {
         hipLaunchKernelGGL(lz4_compress_kernel<SDFS_CDC_LZ4_V19>, dim3((uint32_t)grid), dim3(64), 0, s, a);
     } else {
@@ -648,6 +706,9 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     z->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char* v = getenv("SDFS_LZ4_GTAB")) z->gtab_mode = atoi(v);
     if (z->gtab_mode) z->wg_per_cu = 24;
+    if (const char* v = getenv("SDFS_LZ4_STAGE")) z->stage = atoi(v);
+    if (z->stage != 16384 && z->stage != 32768) z->stage = 0;
+    if (z->stage) z->wg_per_cu = z->stage == 32768 ? 3 : 4;  // 16 KiB table + 1 KiB scratch + stage per workgroup
     if (const char* v = getenv("SDFS_LZ4_WG_PER_CU")) z->wg_per_cu = std::max(1, atoi(v));
     if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
         delete z;
