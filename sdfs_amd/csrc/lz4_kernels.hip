@@ -455,14 +455,19 @@ __device__ uint32_t decompress_block(SrcPtr __restrict__ src, uint32_t n, uint8_
     }
 }
 
-constexpr uint32_t kDecStage = 8192;  // compressed bytes staged in LDS per wave (larger blocks parse from global)
-constexpr int kDecWgPerCu = 16;
+// compressed bytes staged in LDS per wave (larger blocks parse from global) and workgroups per CU:
+// 4 KiB x 28 decodes text 12 % faster than 8 KiB x 16 (more blocks in flight outweigh the blocks
+// that parse from global; profiles/r01/lz4_dec_sweep.jsonl).  SDFS_LZ4_DEC_STAGE=8192 /
+// SDFS_LZ4_DEC_WG_PER_CU select the others for measurements.
+constexpr uint32_t kDecStage = 4096;
+constexpr int kDecWgPerCu = 28;
 
 // a block: staged through LDS when it fits (the token/length/offset parse and the literal reads
 // become LDS round trips), else parsed from global memory
+template <uint32_t STAGE>
 __device__ __forceinline__ uint32_t decode_any(const uint8_t* in, uint32_t n, uint8_t* o, uint32_t cap, uint8_t* stage,
                                                uint32_t lane) {
-    if (n <= kDecStage) {
+    if (n <= STAGE) {
         copy_bytes(stage, in, n, lane);
         __builtin_amdgcn_s_waitcnt(0);  // staged bytes written before any lane parses them
         return decompress_block((lds_cu8*)stage, n, o, cap, lane);
@@ -470,8 +475,9 @@ __device__ __forceinline__ uint32_t decode_any(const uint8_t* in, uint32_t n, ui
     return decompress_block(in, n, o, cap, lane);
 }
 
+template <uint32_t STAGE = kDecStage>
 __global__ __launch_bounds__(64) void lz4_decompress_kernel(Lz4DecArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kDecStage + 16];  // + the realigning reads' spare dword
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE + 16];  // + the realigning reads' spare dword
     const uint32_t lane = threadIdx.x;
     const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
     for (uint64_t c = blockIdx.x; c < n_items; c += gridDim.x) {
@@ -488,7 +494,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(Lz4DecArgs a) {
                 in += 4;
                 n -= 4;
                 if (nz > 0) {
-                    got = (uint32_t)nz <= cap ? decode_any(in, n, o, (uint32_t)nz, stage, lane) : kLz4Corrupt;
+                    got = (uint32_t)nz <= cap ? decode_any<STAGE>(in, n, o, (uint32_t)nz, stage, lane) : kLz4Corrupt;
                     if (got != (uint32_t)nz) got = kLz4Corrupt;
                 } else if (n <= cap) {
                     copy_bytes(o, in, n, lane);
@@ -498,7 +504,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(Lz4DecArgs a) {
                 }
             }
         } else {
-            got = decode_any(in, n, o, cap, stage, lane);
+            got = decode_any<STAGE>(in, n, o, cap, stage, lane);
         }
         if (lane == 0) a.dst_len[c] = got;
     }
@@ -631,6 +637,8 @@ struct sdfs_cdc_lz4 {
     int wg_per_cu = kLz4WgPerCu;  // SDFS_LZ4_WG_PER_CU overrides (measurements)
     int gtab_mode = 0;            // SDFS_LZ4_GTAB=1: hash tables in global memory
     int stage = 0;                // SDFS_LZ4_STAGE=16384|32768: chunks up to that size staged in LDS
+    int dec_stage = (int)kDecStage;
+    int dec_wg_per_cu = kDecWgPerCu;
     ZBuf<uint32_t> gtab;
     hipStream_t stream = nullptr;
     ZBuf<uint64_t> bsum;
@@ -709,6 +717,8 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     if (const char* v = getenv("SDFS_LZ4_STAGE")) z->stage = atoi(v);
     if (z->stage != 16384 && z->stage != 32768) z->stage = 0;
     if (z->stage) z->wg_per_cu = z->stage == 32768 ? 3 : 4;  // 16 KiB table + 1 KiB scratch + stage per workgroup
+    if (const char* v = getenv("SDFS_LZ4_DEC_STAGE")) z->dec_stage = atoi(v) == 8192 ? 8192 : (int)kDecStage;
+    if (const char* v = getenv("SDFS_LZ4_DEC_WG_PER_CU")) z->dec_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_WG_PER_CU")) z->wg_per_cu = std::max(1, atoi(v));
     if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
         delete z;
@@ -842,9 +852,13 @@ int sdfs_cdc_lz4_decompress_device(sdfs_cdc_lz4* z, const uint8_t* d_src, const 
     std::lock_guard<std::mutex> lk(z->mu);
     LZ_TRY(hipSetDevice(z->device));
     Lz4DecArgs a{d_src, d_src_off, d_src_len, d_count, n_max, d_out, d_dst_off, d_dst_cap, d_dst_len, framed ? 1u : 0u};
-    const uint64_t grid = std::min<uint64_t>(n_max, (uint64_t)z->num_cus * kDecWgPerCu);
-    hipLaunchKernelGGL(lz4_decompress_kernel, dim3((uint32_t)grid), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
-                       a);
+    const uint64_t grid = std::min<uint64_t>(n_max, (uint64_t)z->num_cus * z->dec_wg_per_cu);
+    if (z->dec_stage == 8192)
+        hipLaunchKernelGGL(lz4_decompress_kernel<8192>, dim3((uint32_t)grid), dim3(64), 0,
+                           reinterpret_cast<hipStream_t>(stream), a);
+    else
+        hipLaunchKernelGGL(lz4_decompress_kernel<kDecStage>, dim3((uint32_t)grid), dim3(64), 0,
+                           reinterpret_cast<hipStream_t>(stream), a);
     LZ_TRY(hipGetLastError());
     return SDFS_CDC_OK;
 }
@@ -865,7 +879,7 @@ int sdfs_cdc_lz4_decompress(sdfs_cdc_lz4* z, const uint8_t* src, uint32_t n, uin
     LZ_TRY(hipMemcpyAsync(z->h_slen.p, lens, sizeof(lens), hipMemcpyHostToDevice, s));
     Lz4DecArgs a{z->h_in.p, z->h_soff.p, z->h_slen.p, nullptr, 1, z->h_out.p, z->h_soff.p + 1, z->h_slen.p + 1,
                  z->h_slen.p + 2, 0};
-    hipLaunchKernelGGL(lz4_decompress_kernel, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(lz4_decompress_kernel<kDecStage>, dim3(1), dim3(64), 0, s, a);
     LZ_TRY(hipGetLastError());
     uint32_t got = 0;
     LZ_TRY(hipMemcpyAsync(&got, z->h_slen.p + 2, 4, hipMemcpyDeviceToHost, s));
