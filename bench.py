@@ -46,6 +46,17 @@ def cpu_baseline(target_secs: float, threads: int):
                        f"{nbytes / max(chunks, 1):.0f} B mean chunk; CPU restatement, not the Java reference")
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def load_traffic(name: str):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -67,6 +78,7 @@ def main():
     ap.add_argument("--buf-kib", type=int, default=256, help="CHUNK_LENGTH in KiB")
     ap.add_argument("--cpu-secs", type=float, default=12.0, help="CPU baseline sample size (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-1t-secs", type=float, default=3.0, help="single-thread CPU baseline sample (0 = skip)")
     ap.add_argument("--e2e-mib", type=int, default=1024, help="host->GPU->host measurement size (0 = skip)")
     ap.add_argument("--min-seg-kib", type=int, default=4,
                     help="min-variable-segment-size (minLen = KiB*1024-1; 4 = the reference default)")
@@ -234,6 +246,10 @@ def main():
         th = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         log(f"cpu baseline: {th} threads, ~{args.cpu_secs}s sample")
         cpu = cpu_baseline(args.cpu_secs, th)
+        if th > 1 and args.cpu_1t_secs > 0:  # T = all cores and T = 1
+            one = cpu_baseline(args.cpu_1t_secs, 1)
+            cpu["one_thread"] = {"value": one["value"], "sample": one["sample"]}
+        cpu["cpu_model"] = cpu_model()
     res = {
         "metric": "device-resident GiB/s CDC+fingerprint, 4 KiB-mean chunks, 1/2/4/8 MI355X",
         "value": round(value, 3),
