@@ -39,9 +39,10 @@ __device__ __forceinline__ uint32_t bitop3_and_or(uint32_t a, uint32_t b, uint32
 // pushByte/popByte pair:
 //   j = (fp >> (d-8)) & 0xFF;  fp = ((fp << 8) | b) ^ push[j];  fp ^= pop[o]
 // push[j] carries j*x^d, which cancels the 8 bits shifted above deg-1.
-// Ablation bits (scan sweeps only; production ABL = 0): 1 = no pop LDS read, 2 = no push LDS
-// read, 4 = no candidate test, 8 = no global loads.  The skipped values are replaced by register
-// values that keep every remaining instruction live.
+// Ablation bits (scan sweeps only): 1 = no pop LDS read, 2 = no push LDS read, 4 = no candidate
+// test, 8 = no global loads.  The skipped values are replaced by register values that keep every
+// remaining instruction live.  Bit 16 is not an ablation but a code layout (production): whole
+// blocks are loaded and scanned in a branch of their own (see the scan kernel's block loop).
 template <int P, int Q, int ABL = 0>
 __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
                                           uint32_t push_base, uint32_t jshift, const uint8_t* tab) {
@@ -489,6 +490,32 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
         for (uint32_t blk = 0; blk < maxblk; blk++) {
             uint32_t nxt[NCH][CFG::kPrefetch ? BLKW : 1];
             bool nxt_full[NCH];
+            uint32_t words[NCH][BLK / 32];
+            bool split_fast = false;
+            if constexpr (CFG::kAbl & 16) {
+                // split body: when every lane's block is whole, a branch of its own loads and
+                // scans it, so no control-flow merge sits between the loads and their uses (hipcc
+                // waits for all 16 loads at such a merge; here it waits per 64 bytes scanned).
+                // Interleaved A/B: 1.59 -> 1.52 ms per 4 GiB (profiles/r01/probes/scan_split_body_ab.jsonl)
+                bool full = true;
+#pragma unroll
+                for (int c = 0; c < NCH; c++)
+                    full = full && blk < nblk[c] && start[c] + (uint64_t)BLK * (blk + 1) <= end[c];
+                split_fast = __all(full);
+                if (split_fast) {
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        const uint4* p = reinterpret_cast<const uint4*>(a.data + start[c] + (uint64_t)BLK * blk);
+#pragma unroll
+                        for (int i = 0; i < BLKW / 4; i++) {
+                            const uint4 v = p[i];
+                            cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
+                        }
+                    }
+                    block_words<W, PRED64, 0, BLK / 32, NCH, 0, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+                }
+            }
+            if (!split_fast) {
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 if constexpr (CFG::kPrefetch) {
@@ -504,8 +531,8 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
                     load_block<BLKW>(cur[c], a.data, act ? start[c] + (uint64_t)BLK * blk : 0, act ? end[c] : 0);
                 }
             }
-            uint32_t words[NCH][BLK / 32];
-            block_words<W, PRED64, 0, BLK / 32, NCH, CFG::kAbl, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+            block_words<W, PRED64, 0, BLK / 32, NCH, CFG::kAbl & 15, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+            }
             if constexpr (CFG::kFuse == 2) {
                 // candidates are rare (~1 per 4 KiB): a divergent, seldom-taken append
 #pragma unroll
@@ -577,7 +604,8 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
 // 32 conflict-free table copies, one segment per lane, two whole 128-byte lines per lane per
 // iteration (interleaved A/B on MI355X, scripts/ab.py: 1.56 ms / 4 GiB vs 1.78 ms with one line
 // (variant 7) and 2.6 ms with 64-byte loads; DESIGN.md "Scan variants").
-using ScanV0 = ScanCfg<32, 1, false, 4, 0, 256, 2>;  // + cut resolution from register summaries
+using ScanV0 = ScanCfg<32, 1, false, 4, 16, 256, 2>;  // + split fast-path body (ABL bit 16, below)
+using ScanV21 = ScanCfg<32, 1, false, 4, 0, 256, 2>;  // + cut resolution from register summaries
 using ScanV20 = ScanCfg<32, 1, false, 4, 0, 256>;    // production before the fused resolve
 using ScanV16 = ScanCfg<32, 2, false, 4>;  // round-1 first version: 64-byte loads, 2 chains
 using ScanV17 = ScanCfg<32, 2, true, 4, 0, 128>;
@@ -625,6 +653,7 @@ ScanVariantInfo scan_variant_info(int v) {
     case 17: return info_of<ScanV17>();
     case 19: return info_of<ScanV19>();
     case 20: return info_of<ScanV20>();
+    case 21: return info_of<ScanV21>();
     case 11: return info_of<ScanA1>();
     case 12: return info_of<ScanA2>();
     case 13: return info_of<ScanA3>();
@@ -663,12 +692,13 @@ static hipError_t launch_scan_c(const ScanArgs& a, int window, bool pred64, int 
 hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t s) {
     switch (variant) {
     case 0: return launch_scan_c<ScanV0>(a, window, pred64, grid, s);
+
 #ifdef SDFS_SCAN_SWEEP
 #define SWEEP_CASE(id, T) \
     case id: return window == 48 ? launch_scan_wc<48, T>(a, pred64, grid, s) : hipErrorInvalidValue;
     SWEEP_CASE(1, ScanV1) SWEEP_CASE(2, ScanV2) SWEEP_CASE(3, ScanV3) SWEEP_CASE(4, ScanV4)
     SWEEP_CASE(5, ScanV5) SWEEP_CASE(6, ScanV6) SWEEP_CASE(7, ScanV7) SWEEP_CASE(8, ScanV8)
-    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16) SWEEP_CASE(17, ScanV17) SWEEP_CASE(19, ScanV19) SWEEP_CASE(20, ScanV20) SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3)
+    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16) SWEEP_CASE(17, ScanV17) SWEEP_CASE(19, ScanV19) SWEEP_CASE(20, ScanV20) SWEEP_CASE(21, ScanV21) SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3)
     SWEEP_CASE(14, ScanA4) SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15)
 #undef SWEEP_CASE
 #endif
