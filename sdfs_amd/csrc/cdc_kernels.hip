@@ -329,8 +329,8 @@ __device__ __forceinline__ void sum_push(uint32_t (&s)[4], uint32_t& ncand, uint
 // the first lane whose segment holds one there.  A step whose range touches an overflowed
 // segment searches the bitmap instead (same answer; the bitmap is complete).
 __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint32_t b, uint32_t lane,
-                                                     const uint32_t (&sm)[4], uint32_t ncand, uint32_t seg_len,
-                                                     uint32_t* lhist) {
+                                                     const uint32_t (&sm)[4], uint32_t ncand, uint32_t ovf_off,
+                                                     uint32_t seg_len, uint32_t* lhist) {
     const uint32_t len = a.uniform_len;
     const uint64_t word0 = ((uint64_t)b * len) >> 5;
     const uint32_t my_base = lane * seg_len;
@@ -340,7 +340,7 @@ __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint3
         const uint32_t v = (sm[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
         cand[k] = v == 0xFFFFu ? 0xFFFFFFFFu : my_base + v;
     }
-    const uint64_t ovf = __ballot(ncand > kSumCands);
+    const bool ovf = ncand > kSumCands;
     uint32_t start = 0, cnt = 0;
     while (start < len) {
         const uint32_t lo = start + a.first_off;
@@ -348,20 +348,28 @@ __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint3
         const uint32_t hi = forced < len - 1 ? forced : len - 1;
         int64_t k = -1;
         if (lo <= hi) {
-            const uint32_t slo = lo / seg_len, shi = hi / seg_len;
-            const uint64_t rng = (shi >= 63 ? ~0ull : ((2ull << shi) - 1)) & (~0ull << slo);
-            if (ovf & rng) {
-                k = find_first(a.bitmap, word0, lo, hi, lane);
-            } else {
-                uint32_t best = 0xFFFFFFFFu;
+            uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
-                for (uint32_t j = 0; j < kSumCands; j++) {
-                    const uint32_t c = cand[j];
-                    if (c >= lo && c <= hi && c < best) best = c;
-                }
-                const uint64_t m = __ballot(best != 0xFFFFFFFFu);
-                if (m) k = (int64_t)__builtin_amdgcn_readlane(best, (int)__builtin_ctzll(m));
+            for (uint32_t j = 0; j < kSumCands; j++) {
+                const uint32_t c = cand[j];
+                if (c >= lo && c <= hi && c < best) best = c;
             }
+            // an overflowed segment's later candidates (after its 8th) are in the bitmap words
+            // the scan stored from block ovf_off on; a summary hit precedes all of them
+            if (ovf && best == 0xFFFFFFFFu) {
+                uint32_t x = my_base + ovf_off > lo ? my_base + ovf_off : lo;
+                const uint32_t seg_hi = my_base + seg_len - 1;
+                const uint32_t to = seg_hi < hi ? seg_hi : hi;
+                while (x <= to) {
+                    uint32_t w = a.bitmap[word0 + (x >> 5)] >> (x & 31);
+                    const uint32_t span = to - x;  // positions x .. to, at most 32 of them in this word
+                    if (span < 31) w &= (2u << span) - 1u;
+                    if (w) { best = x + __builtin_ctz(w); break; }
+                    x = (x | 31u) + 1u;
+                }
+            }
+            const uint64_t m = __ballot(best != 0xFFFFFFFFu);
+            if (m) k = (int64_t)__builtin_amdgcn_readlane(best, (int)__builtin_ctzll(m));
         }
         if (k < 0) k = (int64_t)hi;  // forced cut at max_len, or the tail chunk
         const uint32_t clen = (uint32_t)(k + 1 - start);
@@ -471,6 +479,11 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
         bool cur_full[NCH];
         uint32_t sm[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};  // FUSE == 2: candidate summary
         uint32_t ncand = 0;
+        uint32_t ovf_off = 0xFFFFFFFFu;  // FUSE == 2: segment offset of the first stored bitmap block
+        // FUSE == 2 with the fused resolve: bitmap words are stored only once a lane's summary has
+        // overflowed (> kSumCands candidates), from that block on; resolve_from_summary reads them
+        // only there.  Saves the 0.5 GB of bitmap writes per 4 GiB.
+        const bool sparse_bm = CFG::kFuse == 2 && a.fuse_resolve;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             if (nblk[c] != 0 && !first[c]) {
@@ -547,7 +560,9 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
             }
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
-                if (blk < nblk[c]) {
+                if constexpr (CFG::kFuse == 2)
+                    if (ncand > kSumCands && ovf_off == 0xFFFFFFFFu) ovf_off = blk * BLK;
+                if (blk < nblk[c] && (!sparse_bm || ncand > kSumCands)) {
                     const uint64_t pos = start[c] + (uint64_t)BLK * blk;
                     uint32_t* bm = a.bitmap + (pos >> 5);
                     if (pos + BLK <= end[c]) {
@@ -584,7 +599,7 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 if constexpr (CFG::kFuse == 2) {
                     if (seg0 < total)
-                        resolve_from_summary(a.res, (uint32_t)(seg0 >> 6), lane, sm, ncand, a.seg_len, lhist);
+                        resolve_from_summary(a.res, (uint32_t)(seg0 >> 6), lane, sm, ncand, ovf_off, a.seg_len, lhist);
                 } else {
                     if (seg0 < total) resolve_buffer(a.res, (uint32_t)(seg0 >> 6), lane, lhist);
                 }

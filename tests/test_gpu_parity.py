@@ -196,6 +196,51 @@ def test_device_b1_sample_full_compare():
     _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 64, 0, None)
 
 
+def _dense_candidate_buffers(nbuf: int, buf_len: int) -> np.ndarray:
+    """Random buffers with zero runs: an all-zero window fingerprints to 0, so every position in
+    a run is a candidate and the 4 KiB scan segments it covers hold far more than the 8
+    candidates a lane keeps in registers (the fused resolve then reads the bitmap blocks stored
+    from the overflow on).  Runs start mid-segment, cross segment boundaries, cover whole
+    buffers, and sit inside and beyond the minLen/maxLen windows."""
+    rng = np.random.default_rng(20261016)
+    host = rng.integers(0, 256, nbuf * buf_len, dtype=np.uint8).reshape(nbuf, buf_len)
+    for b in range(nbuf):
+        kind = b % 4
+        if kind == 0:
+            host[b] = 0
+        elif kind == 1:
+            for _ in range(12):
+                o = int(rng.integers(0, buf_len - 4096))
+                host[b, o:o + int(rng.integers(60, 4000))] = 0
+        elif kind == 2:
+            o = int(rng.integers(0, 64)) * 4096 + int(rng.integers(1000, 3000))
+            host[b, o:o + int(rng.integers(20000, 70000))] = 0
+        else:
+            host[b, : int(rng.integers(4000, 9000))] = 0  # dense from the buffer start
+            o = buf_len - int(rng.integers(100, 5000))
+            host[b, o:] = 0  # and up to the end
+    return host
+
+
+def test_device_dense_candidates_segment_overflow():
+    """Uniform 256 KiB batch (fused resolve) where many segments overflow the register summary."""
+    prm = P()
+    e = engine_for(prm)
+    nbuf, buf_len = 64, 262144
+    host = _dense_candidate_buffers(nbuf, buf_len)
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=buf_len)
+    batch.data.copy_(torch.from_numpy(host.reshape(-1)))
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == counts.sum()
+    dl = O.Params(**prm).digest_len
+    for b in range(nbuf):
+        es, el, ed = O.chunk(host[b].tobytes(), O.Params(**prm))
+        c = counts[b]
+        assert st[b, :c].tolist() == es.tolist() and ln[b, :c].tolist() == el.tolist(), b
+        assert (dg[b, :c, :dl] == ed).all(), b
+
+
 def test_device_b1_full_size_properties():
     """BASELINE configs[1] at full size: 64 streams x 64 MiB = 16384 buffers of 256 KiB."""
     prm = P()
