@@ -510,6 +510,7 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
             t_end(e, t, spost);
         }
         HashArgs ha{};
+    ha.zero_page = e->zero_page.p;
         ha.data = data_p;
         ha.offs = d_offs;
         ha.uniform_len = uniform_len;
@@ -981,6 +982,7 @@ int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uin
     if (len) HIP_TRY(hipMemcpyAsync(e->h_data.p, e->pin_data, len, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(e->o_starts.p, ctl, 16, hipMemcpyHostToDevice, s));
     HashArgs ha{};
+    ha.zero_page = e->zero_page.p;
     ha.data = e->h_data.p;
     ha.uniform_len = 64;  // buffer 0 at offset 0
     ha.starts = e->o_starts.p;
@@ -1009,6 +1011,7 @@ int hash_extents(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_of
                   sc + 1024, sc, sc + 512};
     HIP_TRY(launch_extent_order(xa, s));
     HashArgs ha{};
+    ha.zero_page = e->zero_page.p;
     ha.data = d_data;
     ha.offs = d_offs;
     ha.uniform_len = 0;

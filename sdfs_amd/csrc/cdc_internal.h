@@ -121,6 +121,7 @@ struct HashArgs {
     uint32_t algo;             // SDFS_CDC_SHA256 / _SHA256_160 / _MD5
     uint32_t persist_grid;     // workgroups of the persistent variant (0 = not used)
     uint32_t* wave_ctr;        // [1] zeroed task counter of the persistent variant
+    const uint8_t* zero_page;  // 256 zero bytes: target of the branch-free next-block load past a chunk's last whole block
 };
 
 // Longest-first order of arbitrary chunk extents (getHash in bulk): tasks[] = extent indices,

@@ -1316,15 +1316,31 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
     }
     // One compression per block; lanes of a wave hold chunks of near-equal block count
     // (longest-first binning), so the data/tail branch below is wave-uniform almost always.
+    // ABL bit 16 (with PF): the next block's load is unconditional (the zero page past the last
+    // whole block), so the loop-carried registers need no copy at the data/tail merge; with the
+    // load inside the branch, hipcc copied the new block into place before the compression and
+    // so waited for it there (s_waitcnt vmcnt right after issuing: no prefetch at all).
+    constexpr bool kPF2 = PF && (ABL & 16);
     uint4 nx[4];
-    if constexpr (PF) {
+    if constexpr (kPF2) {
+        load_block64(nx, nfull ? p : a.zero_page);
+    } else if constexpr (PF) {
         if (nfull) load_block64(nx, p);  // block 0 (a chunk shorter than 64 B has none to read)
     }
     for (uint32_t blk = 0; blk < nblocks; blk++) {
         uint32_t w[16];
+        uint4 pf_cur[4];
+        if constexpr (kPF2) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) pf_cur[q] = nx[q];
+            load_block64(nx, blk + 1 < nfull ? p + 64 * (blk + 1) : a.zero_page);
+        }
         if (blk < nfull) {
             uint4 cur[4];
-            if constexpr (PF) {
+            if constexpr (kPF2) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) cur[q] = pf_cur[q];
+            } else if constexpr (PF) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) cur[q] = nx[q];
                 // next block, clamped to the last full one so the load stays branch-free and in bounds
@@ -1461,19 +1477,22 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
         case 15: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
         case 16: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         case 10: hipLaunchKernelGGL((chunk_hash_kernel<0, 4, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+        // the prefetch before ABL bit 16 (its copy at the data/tail merge waited for the load)
+        case 20: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
 #endif
     if (variant != 0) return hipErrorInvalidValue;
-    // production: next-block prefetch (measured ~5 % faster on the B1 length mix, 108 VGPRs) and
+    // production: next-block prefetch, issued unconditionally (ABL bit 16: interleaved A/B 2.762 ->
+    // 2.744 ms median, 2.725 -> 2.680 min, profiles/r01/probes/hash_true_prefetch_ab.jsonl) (measured ~5 % faster on the B1 length mix, 108 VGPRs) and
     // issue priority for waves of long chunks (interleaved A/B: 2.75 vs 2.81 ms per 4 GiB,
     // profiles/r01/probes/hash_prio_ab.jsonl; sweep variant 9 = without)
     switch (a.algo) {
-    case 0: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((chunk_hash_kernel<1, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((chunk_hash_kernel<2, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((chunk_hash_kernel<0, 16, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((chunk_hash_kernel<1, 16, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((chunk_hash_kernel<2, 16, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
