@@ -1,35 +1,55 @@
-# Builds the MI355X (gfx950) engine library and the CPU oracle.  `python -c "import
-# __graft_entry__ as g; g.build()"` runs the same steps.
+# Builds the MI355X (gfx950) engine library, the measurement (tuning) library and the CPU
+# oracle.  `python -c "import __graft_entry__ as g; g.build()"` runs the same steps.
+#   sdfs_amd/libsdfs_cdc.so         the product: production kernels only, reads no environment
+#   sdfs_amd/libsdfs_cdc_tuning.so  the same C-ABI plus the measured kernel variants and the
+#                                   SDFS_* A/B switches (-DSDFS_TUNING; scripts/, variant tests)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
 CSRC := sdfs_amd/csrc
 LIB := sdfs_amd/libsdfs_cdc.so
-OBJS := build/cdc_kernels.o build/cdc_engine.o build/dedup_index.o build/lz4_kernels.o build/map_emit.o build/aes_kernels.o
-SWEEP_LIB := sdfs_amd/libsdfs_cdc_sweep.so
+TUNING_LIB := sdfs_amd/libsdfs_cdc_tuning.so
+SRCS := cdc_kernels cdc_engine dedup_index lz4_kernels map_emit aes_kernels
+OBJS := $(SRCS:%=build/%.o)
+TUNING_OBJS := $(SRCS:%=build/tuning/%.o) build/tuning/cdc_sweep.o
+HDRS := $(CSRC)/cdc_internal.h $(CSRC)/cdc_device.h $(CSRC)/host_queue.h $(wildcard include/*.h)
 
-all: $(LIB) oracle
+all: $(LIB) tuning tools oracle
 
-# kernel-variant sweep build (scripts/sweep_scan.py); not used by the product path
-sweep: $(SWEEP_LIB)
-build/sweep_kernels.o: $(CSRC)/cdc_kernels.hip $(CSRC)/cdc_internal.h
-	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -DSDFS_SCAN_SWEEP -c $< -o $@
-$(SWEEP_LIB): build/sweep_kernels.o build/cdc_engine.o build/dedup_index.o build/lz4_kernels.o build/map_emit.o build/aes_kernels.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+tuning: $(TUNING_LIB)
 
-build/%.o: $(CSRC)/%.hip $(CSRC)/cdc_internal.h include/sdfs_cdc.h include/sdfs_index.h include/sdfs_lz4.h include/sdfs_meta.h include/sdfs_aes.h
+build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+build/tuning/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p build/tuning
+	$(HIPCC) $(HIPFLAGS) -DSDFS_TUNING -c $< -o $@
+
 $(LIB): $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+
+$(TUNING_LIB): $(TUNING_OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(TUNING_OBJS)
+
+# host-side harnesses: the multi-threaded getChunks driver (bench.py, GPU tests) and the JNI glue
+tools: tools/libsdfs_threads.so jni/libsdfs_cdc_jni.so tests/jni/libjni_stub.so
+
+tools/libsdfs_threads.so: tools/threads_bench.c include/sdfs_cdc.h $(LIB)
+	gcc -O2 -std=c11 -fPIC -shared -Wall -Wextra -D_GNU_SOURCE -o $@ $< -Lsdfs_amd -lsdfs_cdc -Wl,-rpath,'$$ORIGIN/../sdfs_amd' -lpthread
+
+jni/libsdfs_cdc_jni.so: jni/sdfs_cdc_jni.c jni/jni_min.h include/sdfs_cdc.h $(LIB)
+	gcc -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ $< -Lsdfs_amd -lsdfs_cdc -Wl,-rpath,'$$ORIGIN/../sdfs_amd'
+
+# test infrastructure: a stand-in JNIEnv for driving the JNI glue without a JVM (tests/test_jni.py)
+tests/jni/libjni_stub.so: tests/jni/jni_stub.c jni/jni_min.h
+	gcc -O2 -std=gnu11 -fPIC -shared -Wall -Wextra -o $@ $<
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(TUNING_LIB) tools/*.so jni/*.so tests/jni/*.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean sweep
+.PHONY: all oracle clean tuning tools

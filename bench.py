@@ -9,11 +9,16 @@ One step = scan + cut resolution + SHA-256 of every chunk of the 4 GiB; at N > 1
 all-gathers the fingerprint table (48-byte records) over RCCL (sdfs_amd/dist.py).  Weak scaling:
 rank r owns streams [64r, 64r+64).
 
+Production device path: one engine, steps alternating between two HIP streams (the engine's
+workspace ring keeps two batches in flight, so one batch's scan fills the tail of the other's
+fingerprinting).  The one-stream rate is reported beside it (`one_stream`).
+
 Prints ONE JSON line on rank 0 (contract in the task statement); diagnostics go to stderr.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -22,28 +27,32 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz int32 ops/s
-# VALU ops per input byte from the kernels' ISA (DESIGN.md "Roofline"): scan ~11.5, SHA-256 ~21.9
-OPS_PER_BYTE = {"cdc_scan": 11.5, "chunk_hash": 21.9}
+# VALU instructions per input byte, counted in the production ISA: scan 10 per byte
+# (+ block overhead), SHA-256 1383 per 64-byte block + one padding block per chunk
+OPS_PER_BYTE = {"cdc_scan": 10.2, "chunk_hash": 21.9}
+METRIC = "device-resident GiB/s CDC+fingerprint, 4 KiB-mean chunks, 1/2/4/8 MI355X"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(target_secs: float, threads: int):
-    """The CPU oracle (scalar C restatement, oracle/cdc_ref.c) on a bounded sample of the same
-    synthetic workload, timed on this host's cores: a reported baseline, not the target."""
+def cpu_baseline(target_secs: float, threads: int, p_kw: dict):
+    """The CPU restatement of the path (oracle/cdc_fast.c: table-driven Rabin loop + OpenSSL
+    EVP SHA-256, i.e. SHA-NI on this host as HotSpot's intrinsic would use) on a bounded sample of
+    the same synthetic workload, timed on this host's cores: a reported baseline, not the target."""
     from oracle import cdc_oracle as O
 
-    p = O.Params()
-    t_cal, _, by = O.bench_synth(p, threads * 2, 262144, threads)
+    p = O.Params(**p_kw)
+    t_cal, _, by = O.bench_fast(p, threads * 2, 262144, threads)
     rate = by / max(t_cal, 1e-6)
     nbuf = max(threads * 4, int(rate * target_secs / 262144) // threads * threads)
-    secs, chunks, nbytes = O.bench_synth(p, nbuf, 262144, threads, buffers_per_stream=256)
+    secs, chunks, nbytes = O.bench_fast(p, nbuf, 262144, threads, buffers_per_stream=256)
     return dict(value=round(nbytes / secs / 2**30, 4), unit="GiB/s", cores=threads, kind="port",
                 sample=f"{nbuf} x 256 KiB synthetic write buffers (streams 0..{(nbuf - 1) // 256}, "
-                       f"same generator/params), SHA-256, {threads} threads, {secs:.1f} s, "
-                       f"{nbytes / max(chunks, 1):.0f} B mean chunk; CPU restatement, not the Java reference")
+                       f"same generator/params), {threads} threads, {secs:.1f} s, "
+                       f"{nbytes / max(chunks, 1):.0f} B mean chunk; table-driven Rabin + OpenSSL SHA-256 "
+                       f"(CPU restatement, not the Java reference)")
 
 
 def cpu_model() -> str:
@@ -57,15 +66,93 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def load_traffic(name: str):
+def load_traffic(name: str, params: str):
+    """HBM bytes per launch of `name` from the committed PMC passes (profiles/pmc_traffic.json),
+    only when they were measured on this exact configuration; with the source label."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
     try:
         d = json.load(open(path))
-        return d.get(name, {}).get("hbm_bytes_per_launch")
     except Exception:
-        return None
+        return None, None
+    if d.get("params") != params or name not in d:
+        return None, None
+    return d[name].get("hbm_bytes_per_launch"), f"{d.get('source', '?')} (commit {d.get('commit', '?')})"
+
+
+def git_head() -> str:
+    try:
+        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or "unknown"
+    except Exception:
+        return "unknown"
+
+
+class TwoStreamRunner:
+    """Steps alternate between two HIP streams on ONE engine, each with its own output set
+    (DeviceBatch) over the same resident input: two batches in flight."""
+
+    def __init__(self, torch, eng, batch, cs, DeviceBatch, nbuf, buf_len, device):
+        self.torch = torch
+        self.batches = [batch, DeviceBatch(eng, nbuf=nbuf, buf_len=buf_len, device=device)]
+        self.batches[1].data = batch.data
+        self.streams = [cs, torch.cuda.Stream(device=device)]
+        self.k = 0
+
+    def step(self, buffer_id_base, exchange=None):
+        i = self.k & 1
+        self.k += 1
+        b, s = self.batches[i], self.streams[i]
+        b.run(buffer_id_base=buffer_id_base, stream=s.cuda_stream)
+        if exchange is not None:
+            exchange.submit(b.recs.view(-1, 48), b.total, stream=s)
+
+    def identical(self) -> bool:
+        t = self.torch
+        t.cuda.synchronize()
+        a, b = self.batches
+        return bool(t.equal(a.record_table(), b.record_table()) and t.equal(a.counts, b.counts))
+
+
+def timed(torch, dist, world, fn, steps):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    return el
+
+
+def threads_sweep(eng_cfg, device, host, buf_len, thread_counts):
+    """SDFS's own calling pattern: T C threads, each calling getChunks on one 256 KiB buffer at a
+    time through the C-ABI (coalesced into shared GPU passes); rate and per-call latency."""
+    from sdfs_amd import HashFunctionPool
+    from tools import threads as T
+
+    out = {}
+    eng = HashFunctionPool(eng_cfg, device=device).getHashEngine()
+    T.getchunks(eng, 8, host, buf_len, 64)  # warm: queue slots, pinned staging
+    start = eng.queue_stats()
+    for th in thread_counts:
+        calls = max(256, th * 8)
+        r, _ = T.getchunks(eng, th, host, buf_len, calls)
+        b0 = eng.queue_stats()
+        out[str(th)] = {"gibps": round(r.gibps, 3), "p50_us": round(r.p50_us, 1), "p99_us": round(r.p99_us, 1),
+                        "mean_us": round(r.mean_us, 1), "calls": r.calls, "errors": r.first_error}
+        out[str(th)]["_stats"] = b0
+    # batches per sweep point from the cumulative queue statistics
+    prev = start
+    for th in thread_counts:
+        cur = out[str(th)].pop("_stats")
+        nb, nr = cur[0] - prev[0], cur[1] - prev[1]
+        out[str(th)]["calls_per_gpu_pass"] = round(nr / max(nb, 1), 1)
+        prev = cur
+    eng.destroy()
+    return out
 
 
 def main():
@@ -79,15 +166,19 @@ def main():
     ap.add_argument("--cpu-secs", type=float, default=12.0, help="CPU baseline sample size (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-1t-secs", type=float, default=3.0, help="single-thread CPU baseline sample (0 = skip)")
-    ap.add_argument("--e2e-mib", type=int, default=1024, help="host->GPU->host measurement size (0 = skip)")
+    ap.add_argument("--e2e-mib", type=int, default=1024, help="host->GPU->host batch measurement size (0 = skip)")
+    ap.add_argument("--threads", default="1,8,32,128,384",
+                    help="getChunks caller-thread counts for the coalescing-queue sweep ('' = skip)")
     ap.add_argument("--min-seg-kib", type=int, default=4,
                     help="min-variable-segment-size (minLen = KiB*1024-1; 4 = the reference default)")
     ap.add_argument("--mask-bits", type=int, default=12,
                     help="boundary predicate (fp & (2^bits-1)) == 0 (12 = the default knob, SURVEY.md A.3)")
+    ap.add_argument("--at-4k", type=int, default=1, help="also time the 4 KiB-mean mix (minLen 2047, 11-bit)")
     ap.add_argument("--hash-type", default="VARIABLE_SHA256",
                     choices=["VARIABLE_SHA256", "VARIABLE_SHA256_160", "VARIABLE_MD5"])
     ap.add_argument("--ramp-secs", type=float, default=0.3, help="untimed clock ramp before the warmup steps")
-    ap.add_argument("--pipelined", type=int, default=1, help="also time two batches in flight (N = 1)")
+    ap.add_argument("--streams-in-flight", type=int, default=2, choices=[1, 2],
+                    help="HIP streams the steps alternate on (2 = production: two batches in flight)")
     ap.add_argument("--exchange", type=int, default=-1,
                     help="record all-gather: -1 = when N > 1, 1 = also at N = 1 (exercises the path)")
     args = ap.parse_args()
@@ -99,14 +190,15 @@ def main():
     import torch.distributed as dist
 
     torch.cuda.set_device(local)
+    device = f"cuda:{local}"
     use_ex = world > 1 if args.exchange < 0 else bool(args.exchange)
-    if use_ex:
+    if use_ex or world > 1:
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dist.init_process_group("nccl", device_id=torch.device(device))
 
     from sdfs_amd import HashFunctionPool, SdfsConfig
     from sdfs_amd.device import DeviceBatch
@@ -119,145 +211,171 @@ def main():
     bufs_per_stream = args.stream_mib * 1024 // args.buf_kib
     streams = shard_streams(args.streams * world, world, rank)
     nbuf = len(streams) * bufs_per_stream
-    batch = DeviceBatch(eng, nbuf=nbuf, buf_len=buf_len, device=f"cuda:{local}")
+    nbytes = nbuf * buf_len
+    batch = DeviceBatch(eng, nbuf=nbuf, buf_len=buf_len, device=device)
     batch.fill_streams(first_stream=streams.start, bufs_per_stream=bufs_per_stream)
     torch.cuda.synchronize()
     cs = torch.cuda.current_stream()
+    base_id = rank * nbuf
+    runner = TwoStreamRunner(torch, eng, batch, cs, DeviceBatch, nbuf, buf_len, device)
+    nsf = args.streams_in_flight
     # N > 1: the one real exchange (all-gather of the fingerprint records), pipelined on a side
-    # stream so step i's tables travel while step i+1 is chunked (sdfs_amd/dist.py)
-    ex = RecordExchange(batch.recs.view(-1, 48).shape[0], f"cuda:{local}") if use_ex else None
-    gathered = [0]
+    # stream so step i's table travels while step i+1 is chunked (sdfs_amd/dist.py)
+    ex = RecordExchange(batch.recs.view(-1, 48).shape[0], device) if use_ex else None
 
     def step():
-        batch.run(buffer_id_base=rank * nbuf, stream=cs.cuda_stream)
-        if ex is not None:
-            ex.submit(batch.recs.view(-1, 48), batch.total, stream=cs)
+        if nsf == 2:
+            runner.step(base_id, ex)
+        else:
+            batch.run(buffer_id_base=base_id, stream=cs.cuda_stream)
+            if ex is not None:
+                ex.submit(batch.recs.view(-1, 48), batch.total, stream=cs)
 
     def drain():
         if ex is not None:
-            res = ex.flush()
-            gathered[0] = sum(cl for _, counts in res[-1:] for cl in counts)
+            ex.flush()
 
     # clock ramp: ~0.3 s of chunking before the W warmup steps (the GPU idles while the host sets
     # up and its clocks drop; a few 4.5 ms steps do not bring them back), outside the timed region
     t_ramp = time.perf_counter()
     while time.perf_counter() - t_ramp < args.ramp_secs:
-        batch.run(buffer_id_base=rank * nbuf, stream=cs.cuda_stream)
+        batch.run(buffer_id_base=base_id, stream=cs.cuda_stream)
         torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    # timed region: HIP events only around the dominant kernel (the roofline's launch duration),
-    # so the per-kernel event pairs of the breakdown do not tax the measured throughput
+    # timed region: HIP events only around the dominant kernel (the roofline's launch duration)
     eng.set_timing_stages(args.steps, ("chunk_hash",))
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+
+    def timed_steps():
+        for _ in range(args.steps):
+            step()
+        drain()
+
+    elapsed = timed(torch, dist, world, timed_steps, 1)
     if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     hash_ms_live = eng.kernel_times().get("chunk_hash", 0.0)
-    # per-stage breakdown (untimed pass, events around every kernel)
+    identical = runner.identical() if nsf == 2 else None
+
+    # per-stage breakdown (untimed, one stream, events around every kernel)
     nbd = max(3, min(args.steps, 10))
     eng.set_timing(nbd)
     for _ in range(nbd):
-        batch.run(buffer_id_base=rank * nbuf, stream=cs.cuda_stream)
+        batch.run(buffer_id_base=base_id, stream=cs.cuda_stream)
     torch.cuda.synchronize()
     kt = eng.kernel_times()
     eng.set_timing(0)
-    kt["chunk_hash"] = hash_ms_live
+    kt_one = dict(kt)
     counts, _, _, _, total = batch.host_results()
 
-    # two batches in flight (N = 1): a second engine alternates with the first on its own stream,
-    # so batch i+1's scan overlaps the tail of batch i's fingerprinting.  Reported beside the
-    # value (which stays the one-stream rate the roofline's launch durations describe).
-    pipelined = None
-    if world == 1 and args.pipelined:
-        eng2 = HashFunctionPool(cfg, device=local).getHashEngine()
-        batch2 = DeviceBatch(eng2, nbuf=nbuf, buf_len=buf_len, device=f"cuda:{local}")
-        batch2.data = batch.data
-        ss = [cs, torch.cuda.Stream()]
-        pair = [batch, batch2]
-        for k in range(2):
-            pair[k].run(stream=ss[k].cuda_stream)
-        torch.cuda.synchronize()
-        tp = time.perf_counter()
-        for i in range(args.steps):
-            pair[i % 2].run(stream=ss[i % 2].cuda_stream)
-        torch.cuda.synchronize()
-        el = time.perf_counter() - tp
-        same = bool(torch.equal(batch2.record_table(), batch.record_table()))
-        pipelined = {"value": round(nbuf * buf_len * args.steps / el / 2**30, 3),
-                     "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps,
-                     "mode": "2 engines, whole batches alternating on 2 streams", "records_identical": same}
-        del batch2
-        eng2.destroy()
+    # the other in-flight mode beside the headline (N = 1 only)
+    other = None
+    if world == 1:
+        def one():
+            batch.run(buffer_id_base=base_id, stream=cs.cuda_stream)
 
-    # end-to-end (pinned host staging + H2D + kernels + D2H), rank 0 only
-    e2e = e2e_pinned = None
-    if rank == 0 and args.e2e_mib > 0:
-        nb = min(nbuf, args.e2e_mib * 1024 // args.buf_kib)
-        host = batch.data[: nb * buf_len].cpu().numpy()
+        def two():
+            runner.step(base_id)
+
+        fn = one if nsf == 2 else two
+        for _ in range(2):
+            fn()
+        el = timed(torch, dist, 1, fn, args.steps)
+        other = {"streams_in_flight": 3 - nsf, "value": round(nbytes * args.steps / el / 2**30, 3),
+                 "ms_per_step": round(el / args.steps * 1e3, 4)}
+
+    # the metric's 4 KiB-mean mix: minLen 2047 (min-variable-segment-size=2) + 11-bit predicate
+    at4k = None
+    if world == 1 and args.at_4k:
+        cfg4 = SdfsConfig(chunk_length=buf_len, min_len=2047, pred_mask=0x7FF, hash_type=args.hash_type)
+        e4 = HashFunctionPool(cfg4, device=local).getHashEngine()
+        b4 = DeviceBatch(e4, nbuf=nbuf, buf_len=buf_len, device=device)
+        b4.data = batch.data
+        r4 = TwoStreamRunner(torch, e4, b4, cs, DeviceBatch, nbuf, buf_len, device)
+        for _ in range(3):
+            r4.step(0)
+        el = timed(torch, dist, 1, lambda: r4.step(0), args.steps)
+        e4.set_timing(nbd)
+        for _ in range(nbd):
+            b4.run(stream=cs.cuda_stream)
+        torch.cuda.synchronize()
+        k4 = e4.kernel_times()
+        e4.set_timing(0)
+        tot4 = int(b4.total.item())
+        at4k = {"value": round(nbytes * args.steps / el / 2**30, 3), "ms_per_step": round(el / args.steps * 1e3, 4),
+                "params": "minLen=2047 (min-variable-segment-size=2) pred=(fp&0x7ff)==0 n>minLen",
+                "mean_chunk_bytes": round(nbytes / max(tot4, 1), 1), "chunks_per_gpu_step": tot4,
+                "kernels_ms": {k: round(v, 4) for k, v in k4.items() if v}, "records_identical": r4.identical()}
+        del r4, b4
+        e4.destroy()
+
+    # host paths (rank 0): the batched C-ABI call and the thread sweep of single-buffer calls
+    e2e = e2e_pinned = sweep = None
+    if rank == 0 and (args.e2e_mib > 0 or args.threads):
         import numpy as np
 
-        offs = np.arange(nb, dtype=np.uint64) * buf_len
-        lens = np.full(nb, buf_len, np.uint32)
-        eng.chunk_batch(host, offs, lens)  # warm (pinned staging allocation)
-        te = time.perf_counter()
-        reps = 3
-        for _ in range(reps):
-            eng.chunk_batch(host, offs, lens)
-        e2e = nb * buf_len * reps / (time.perf_counter() - te) / 2**30
-        # the same from pinned host memory (a JNI direct buffer registered with the driver): the
-        # engine copies to the GPU straight from it, no staging copy
-        hp = torch.empty(nb * buf_len, dtype=torch.uint8, pin_memory=True)
-        hp.copy_(batch.data[: nb * buf_len])
-        hpn = hp.numpy()
-        eng.chunk_batch(hpn, offs, lens)
-        te = time.perf_counter()
-        for _ in range(reps):
+        nb = min(nbuf, max(args.e2e_mib, 256) * 1024 // args.buf_kib)
+        host = batch.data[: nb * buf_len].cpu().numpy()
+        if args.e2e_mib > 0:
+            offs = np.arange(nb, dtype=np.uint64) * buf_len
+            lens = np.full(nb, buf_len, np.uint32)
+            eng.chunk_batch(host, offs, lens)  # warm (pinned staging allocation)
+            te = time.perf_counter()
+            reps = 3
+            for _ in range(reps):
+                eng.chunk_batch(host, offs, lens)
+            e2e = nb * buf_len * reps / (time.perf_counter() - te) / 2**30
+            hp = torch.empty(nb * buf_len, dtype=torch.uint8, pin_memory=True)
+            hp.copy_(batch.data[: nb * buf_len])
+            hpn = hp.numpy()
             eng.chunk_batch(hpn, offs, lens)
-        e2e_pinned = nb * buf_len * reps / (time.perf_counter() - te) / 2**30
-        del hp, hpn
+            te = time.perf_counter()
+            for _ in range(reps):
+                eng.chunk_batch(hpn, offs, lens)
+            e2e_pinned = nb * buf_len * reps / (time.perf_counter() - te) / 2**30
+            del hp, hpn
+        if args.threads:
+            sweep = threads_sweep(cfg, local, host, buf_len, [int(x) for x in args.threads.split(",") if x])
 
     if rank != 0:
-        if use_ex:
+        if dist.is_initialized():
             dist.destroy_process_group()
         return
 
-    nbytes = nbuf * buf_len
     value = world * nbytes * args.steps / elapsed / 2**30
-    dom = max(("cdc_scan", "chunk_hash"), key=lambda k: kt.get(k, 0.0))
-    t_dom = kt.get(dom, 0.0) / 1e3
+    kt["chunk_hash"] = hash_ms_live
+    t_dom = kt.get("chunk_hash", 0.0) / 1e3
     achieved = nbytes / t_dom / 1e9 if t_dom > 0 else 0.0
-    # device time of one pass: the pipeline-level events when present, else the stage sum
-    dev_ms = kt.get("pipeline") or sum(v for k, v in kt.items() if k != "pipeline")
-    valu = {k: round(nbytes * OPS_PER_BYTE[k] / (kt[k] / 1e3) / VALU_PEAK_OPS, 3) for k in OPS_PER_BYTE if kt.get(k)}
+    ms_step = elapsed / args.steps * 1e3
+    valu = {k: round(nbytes * OPS_PER_BYTE[k] / (kt_one[k] / 1e3) / VALU_PEAK_OPS, 3) for k in OPS_PER_BYTE
+            if kt_one.get(k)}
+    params = (f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
+              f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen {args.hash_type}")
+    traffic, traffic_src = load_traffic("chunk_hash", params)
     cpu = None
     if world == 1 and args.cpu_secs > 0:
-        th = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        # the GPU box's CPU share is 16 cores per GPU (the host's nproc shows the whole machine)
+        aff = len(os.sched_getaffinity(0))
+        th = args.cpu_threads or min(16, aff)
+        p_kw = dict(min_len=cfg.min_len, pred_mask=cfg.pred_mask)
         log(f"cpu baseline: {th} threads, ~{args.cpu_secs}s sample")
-        cpu = cpu_baseline(args.cpu_secs, th)
+        cpu = cpu_baseline(args.cpu_secs, th, p_kw)
         if th > 1 and args.cpu_1t_secs > 0:  # T = all cores and T = 1
-            one = cpu_baseline(args.cpu_1t_secs, 1)
+            one = cpu_baseline(args.cpu_1t_secs, 1, p_kw)
             cpu["one_thread"] = {"value": one["value"], "sample": one["sample"]}
         cpu["cpu_model"] = cpu_model()
+        cpu["affinity_cpus"] = aff
     res = {
-        "metric": "device-resident GiB/s CDC+fingerprint, 4 KiB-mean chunks, 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -266,34 +384,41 @@ def main():
         "config": {
             "workload": f"{args.streams} streams x {args.stream_mib} MiB per GPU, CHUNK_LENGTH {buf_len} B "
                         f"({nbuf} buffers, {nbytes / 2**30:.2f} GiB per GPU), fresh CDC state per buffer",
-            "params": f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
-                      f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen {args.hash_type}",
+            "params": params,
             "mean_chunk_bytes": round(nbytes / max(total, 1), 1),
             "chunks_per_gpu_step": total,
+            "streams_in_flight": nsf,
+            "records_identical_across_streams": identical,
             "exchange": "RCCL all_gather of 48-B fingerprint records, pipelined" if use_ex else "none (N=1)",
             "parallelism": f"dp{world} (streams sharded per GPU)",
         },
         "kernels_ms": {k: round(v, 4) for k, v in kt.items()},
-        "kernels_note": "chunk_hash: HIP events on the launch stream over the timed steps; other stages: a "
-                        "separate untimed pass with events around every kernel",
+        "kernels_note": "chunk_hash: HIP events on the launch streams over the timed steps (two batches in "
+                        "flight stretch it); other stages: a separate untimed one-stream pass",
         "roofline": {
             "bound": "hbm",
-            "kernel": dom,
+            "kernel": "chunk_hash",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_traffic(dom),
-            "pipeline_gbps": round(nbytes / (dev_ms / 1e3) / 1e9, 1) if dev_ms else None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "one_stream_kernel_ms": round(kt_one.get("chunk_hash", 0.0), 4),
+            "achieved_per_step": round(nbytes / (ms_step / 1e3) / 1e9, 1),
+            "frac_per_step": round(nbytes / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
             "valu_frac": valu,
         },
         "cpu_baseline": cpu,
+        "one_stream" if nsf == 2 else "two_streams": other,
+        "at_4k_mean": at4k,
         "e2e_host_gibps": round(e2e, 3) if e2e else None,
         "e2e_pinned_host_gibps": round(e2e_pinned, 3) if e2e_pinned else None,
-        "pipelined_2stream": pipelined,
+        "e2e_getchunks_threads": sweep,
+        "commit": git_head(),
     }
     print(json.dumps(res), flush=True)
-    if use_ex:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

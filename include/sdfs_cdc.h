@@ -15,8 +15,11 @@
  * SDFSLogger.fatal + System.exit(5) (HashFunctionPool.java:116-119); the shim decides.
  *
  * Threading: one engine may be shared by all SDFS flush threads (SparseDedupFile.java:100 is a
- * static singleton), so every call is re-entrant and thread-safe (calls are serialised per
- * engine context; see DESIGN.md "Host edge").
+ * static singleton; the flush pools are Main.writeThreads wide, WritableCacheBuffer.java:100-104),
+ * so every call is re-entrant and thread-safe.  Concurrent sdfs_cdc_get_chunks / sdfs_cdc_get_hash
+ * calls are coalesced: each caller copies its bytes into a shared pinned staging slot, one GPU
+ * pass serves the whole slot (up to two passes in flight), and each caller returns with its own
+ * results (DESIGN.md "Host edge").  The product library reads no environment variables.
  */
 #ifndef SDFS_CDC_H
 #define SDFS_CDC_H
@@ -62,9 +65,13 @@ typedef struct sdfs_cdc_params {
     uint32_t min_cmp;       /* enum sdfs_cdc_min_cmp */
     uint32_t hash_algo;     /* enum sdfs_cdc_hash_algo */
     int32_t device;         /* HIP device ordinal */
-    uint32_t flags;         /* reserved, 0 */
+    uint32_t flags;         /* SDFS_CDC_FLAG_*; 0 = defaults */
     uint64_t max_batch_bytes; /* host-batch staging per slot (pinned, two slots); 0 = default 256 MiB */
 } sdfs_cdc_params;
+
+/* flags: serve every getChunks / getHash call with its own GPU round trip instead of coalescing
+ * concurrent callers (A/B measurements; the results are identical). */
+#define SDFS_CDC_FLAG_DIRECT 1u
 
 typedef struct sdfs_cdc_engine sdfs_cdc_engine;
 
@@ -132,9 +139,12 @@ int sdfs_cdc_hash_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64
 
 /* ---- AbstractHashEngine.getChunks(byte[], uuid) (VariableSha256HashEngine.java:71-86) ----
  * One host buffer (1..CHUNK_LENGTH bytes, fresh CDC state).  Writes *count chunks into
- * starts/lens/digests (digest_len bytes each, densely packed), capacity cap entries. */
+ * starts/lens/digests (digest_len bytes each, densely packed), capacity cap entries.
+ * Synchronous for the caller; concurrent callers share GPU passes (see "Threading"). */
 int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, uint32_t* starts,
                         uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count);
+/* Coalescing statistics since create: GPU passes launched and getChunks/getHash calls they served. */
+int sdfs_cdc_queue_stats(sdfs_cdc_engine* e, uint64_t* batches, uint64_t* requests);
 
 /* Batched getChunks over nbuf independent host buffers at base+offs[b], lens[b] (each chunked
  * from fresh state; SURVEY.md 0 "every call starts from a fresh state").  Per-buffer slots of
@@ -148,8 +158,10 @@ int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uin
  * (a multiple of 64) at b*uniform_len — the SDFS write-buffer case (every flushed buffer is
  * CHUNK_LENGTH bytes, WritableCacheBuffer.java:115).  buffer_id_base is added to b in the
  * record table.  stream: the hipStream_t to enqueue on (NULL = the HIP null stream, as in every
- * HIP API).  Asynchronous:
- * returns after enqueueing; d_offs/d_lens are ignored (pass NULL). */
+ * HIP API).  Asynchronous: returns after enqueueing; d_offs/d_lens are ignored (pass NULL).
+ * Runs enqueued on different streams proceed concurrently (the engine keeps a ring of device
+ * workspaces, each reused behind its previous run): alternating two streams keeps two batches
+ * in flight, so one batch's scan fills the tail of the other's fingerprinting. */
 int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs,
                         const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len,
                         uint64_t buffer_id_base, const sdfs_cdc_dev_out* out, void* stream);
@@ -159,12 +171,6 @@ int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_
 int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
                                const uint64_t* d_offs, const uint32_t* d_lens, uint32_t nbuf,
                                uint64_t buffer_id_base, const sdfs_cdc_dev_out* out, void* stream);
-/* Sub-batch pipelining of sdfs_cdc_run_device (uniform layouts): split a batch into up to
- * `parts` (1..16) sub-batches of at least part_min_bytes, so the candidate scan of one overlaps
- * the fingerprinting of the previous on the same CUs (engine-internal streams, joined back to the
- * caller's stream).  parts = 1 runs everything on the caller's stream.  Default 1 (measured
- * slower on MI355X when split) / 512 MiB. */
-int sdfs_cdc_set_pipeline(sdfs_cdc_engine* e, int parts, uint64_t part_min_bytes);
 /* Block until the engine's own stream has drained. */
 int sdfs_cdc_stream_sync(sdfs_cdc_engine* e);
 

@@ -1,0 +1,82 @@
+/*
+ * org.opendedup.hashing.HipVariableSha256HashEngine — AbstractHashEngine backed by the MI355X
+ * engine (libsdfs_cdc.so) through the JNI glue in jni/sdfs_cdc_jni.c.  Source for the SDFS tree
+ * (src/org/opendedup/hashing/); this image has no JDK, so it is not compiled here — the glue's
+ * native side is compiled and tested against a stub JNIEnv (tests/test_jni.py).
+ *
+ * Surface: AbstractHashEngine.java:24-39; behaviour: VariableSha256HashEngine.java:41-121
+ * (VARIABLE_SHA256 / VARIABLE_SHA256_160) and VariableMD5HashEngine.java:37-108 (VARIABLE_MD5).
+ * Selected in HashFunctionPool.getHashEngine() (HashFunctionPool.java:102-121), INTEGRATION.md §1.
+ */
+package org.opendedup.hashing;
+
+import java.io.IOException;
+import java.util.ArrayList;
+import java.util.Arrays;
+import java.util.List;
+
+import org.opendedup.sdfs.Main;
+
+public final class HipVariableSha256HashEngine implements AbstractHashEngine {
+    public static enum HASHTYPE { HASH160, HASH256, MD5 }
+
+    static { System.loadLibrary("sdfs_cdc_jni"); }   // links libsdfs_cdc.so
+
+    private static final long POLY = 10923124345206883L;  // VariableSha256HashEngine.java:41
+    private volatile long handle;                          // sdfs_cdc_engine*
+    private final int hashLen;                             // 32, 20 or 16
+
+    public HipVariableSha256HashEngine(HASHTYPE ht) throws IOException {
+        int algo = ht == HASHTYPE.HASH256 ? 0 : (ht == HASHTYPE.HASH160 ? 1 : 2);  // SDFS_CDC_*
+        handle = nativeCreate(POLY, HashFunctionPool.bytesPerWindow, HashFunctionPool.minLen,
+                HashFunctionPool.maxLen, Main.CHUNK_LENGTH, algo, Integer.getInteger("sdfs.hip.device", 0));
+        hashLen = nativeDigestLen(handle);
+    }
+
+    @Override public boolean isVariableLength() { return true; }
+    @Override public int getMaxLen() { return Main.CHUNK_LENGTH; }                 // :106-109
+    @Override public int getMinLen() { return HashFunctionPool.minLen; }           // :111-114
+    @Override public void setSeed(int seed) { }                                     // :116-120
+    @Override public synchronized void destroy() {
+        if (handle != 0) { nativeDestroy(handle); handle = 0; }
+    }
+
+    @Override public byte[] getHash(byte[] data) {                                  // :58-67
+        byte[] out = new byte[hashLen];
+        nativeGetHash(handle, data, out);   // throws IllegalStateException on a device error
+        return out;
+    }
+
+    /** Thread-safe: SDFS's flush threads share one engine (SparseDedupFile.java:100); concurrent
+     *  calls are coalesced into shared GPU passes inside the library. */
+    @Override public List<Finger> getChunks(byte[] data, String uuid) throws IOException {  // :71-86
+        int cap = nativeSlotCap(handle, data.length);
+        int[] starts = new int[cap], lens = new int[cap];
+        byte[] digests = new byte[cap * hashLen];
+        int n = nativeGetChunks(handle, data, starts, lens, digests);  // IOException on failure
+        ArrayList<Finger> al = new ArrayList<Finger>(n);
+        for (int i = 0; i < n; i++) {
+            Finger f = new Finger(uuid);
+            f.start = starts[i];
+            f.len = lens[i];
+            f.chunk = Arrays.copyOfRange(data, starts[i], starts[i] + lens[i]);  // outlives the buffer
+            f.hash = Arrays.copyOfRange(digests, i * hashLen, (i + 1) * hashLen);
+            al.add(f);
+        }
+        return al;
+    }
+
+    /** Page-locks a direct flush buffer (ByteBuffer.allocateDirect) for in-place H2D copies. */
+    public static void register(java.nio.ByteBuffer direct) throws IOException { nativeRegister(direct); }
+
+    private static native long nativeCreate(long poly, int window, int minLen, int maxLen,
+                                            int chunkLength, int algo, int device) throws IOException;
+    private static native void nativeDestroy(long h);
+    private static native int nativeSlotCap(long h, int len);
+    private static native int nativeDigestLen(long h);
+    private static native int nativeGetChunks(long h, byte[] data, int[] starts, int[] lens,
+                                              byte[] digests) throws IOException;
+    private static native int nativeGetHash(long h, byte[] data, byte[] out);
+    private static native int nativeRegister(java.nio.ByteBuffer direct) throws IOException;
+    private static native String nativeLastError();
+}

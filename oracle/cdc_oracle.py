@@ -28,6 +28,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libcdc_ref.so")
+FAST_LIB_PATH = os.path.join(HERE, "libcdc_fast.so")  # cdc_fast.c: bench.py's CPU baseline
 
 SHA256, SHA256_160, MD5 = 0, 1, 2
 MIN_GT, MIN_GE = 0, 1
@@ -114,6 +115,54 @@ def lib():
 
 def _p(a: np.ndarray, ct):
     return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+_fast = None
+
+
+def fast_lib():
+    """oracle/libcdc_fast.so: the table-driven loop + OpenSSL SHA-256/MD5 (CPU baseline form)."""
+    global _fast
+    if _fast is None:
+        lib()  # its dependency libcdc_ref.so first
+        L = ctypes.CDLL(FAST_LIB_PATH)
+        P = ctypes.POINTER
+        u8p, u32p, u64p = P(ctypes.c_uint8), P(ctypes.c_uint32), P(ctypes.c_uint64)
+        L.cdc_fast_chunk.argtypes = [P(CdcRefParams), u8p, ctypes.c_size_t, u32p, u32p, u8p, ctypes.c_size_t]
+        L.cdc_fast_chunk.restype = ctypes.c_long
+        L.cdc_fast_bench_synth.argtypes = [P(CdcRefParams), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, u64p, u64p]
+        L.cdc_fast_bench_synth.restype = ctypes.c_double
+        _fast = L
+    return _fast
+
+
+def chunk_fast(data: bytes | np.ndarray, p: Params | None = None):
+    """cdc_fast_chunk: same contract as chunk() (checked against it in tests/test_oracle.py)."""
+    p = p or Params()
+    a = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data,
+                             np.uint8)
+    cap = p.slot_cap(len(a))
+    st = np.zeros(cap, np.uint32)
+    ln = np.zeros(cap, np.uint32)
+    dg = np.zeros((cap, p.digest_len), np.uint8)
+    cp = p.to_c()
+    n = fast_lib().cdc_fast_chunk(ctypes.byref(cp), _p(a, ctypes.c_uint8), len(a), _p(st, ctypes.c_uint32),
+                                  _p(ln, ctypes.c_uint32), _p(dg, ctypes.c_uint8), cap)
+    if n < 0:
+        raise RuntimeError("cdc_fast_chunk failed")
+    return st[:n].copy(), ln[:n].copy(), dg[:n].copy()
+
+
+def bench_fast(p: Params, nbuf: int, buf_len: int, nthreads: int, seed: int = SYNTH_SEED,
+               stream0: int = 0, buffers_per_stream: int = 256):
+    """CPU baseline (fast form): returns (seconds, chunks, bytes) for chunk+hash of nbuf buffers."""
+    ch = ctypes.c_uint64()
+    by = ctypes.c_uint64()
+    cp = p.to_c()
+    secs = fast_lib().cdc_fast_bench_synth(ctypes.byref(cp), seed, stream0, buffers_per_stream, nbuf, buf_len,
+                                           nthreads, ctypes.byref(ch), ctypes.byref(by))
+    return secs, ch.value, by.value
 
 
 # ---------------------------------------------------------------- C oracle wrappers

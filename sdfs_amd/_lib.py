@@ -11,14 +11,17 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# SDFS_CDC_LIB selects an alternative in-tree build (kernel-variant sweeps, scripts/sweep_scan.py)
+# SDFS_CDC_LIB selects the in-tree measurement build (libsdfs_cdc_tuning.so: kernel-variant
+# sweeps and A/B switches, scripts/sweep_scan.py); the default is the product library
 DEFAULT_LIB = os.path.join(HERE, "libsdfs_cdc.so")
+TUNING_LIB = os.path.join(HERE, "libsdfs_cdc_tuning.so")
 LIB_PATH = os.environ.get("SDFS_CDC_LIB") or DEFAULT_LIB
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "sdfs_cdc.h")
 HEADER_PATHS = [HEADER_PATH] + [os.path.join(os.path.dirname(HERE), "include", h)
                                for h in ("sdfs_index.h", "sdfs_lz4.h", "sdfs_meta.h", "sdfs_aes.h")]
 
 OK, EINVAL, ECAP, EHIP, ENOMEM, ENODEV = 0, -1, -2, -3, -4, -5
+FLAG_DIRECT = 1  # SDFS_CDC_FLAG_DIRECT: no coalescing of concurrent getChunks/getHash calls
 SHA256, SHA256_160, MD5 = 0, 1, 2
 MIN_GT, MIN_GE = 0, 1
 RECORD_BYTES = 48
@@ -89,7 +92,7 @@ SIGNATURES = {
     "sdfs_cdc_run_device_ragged": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32,
                                                   ctypes.c_uint64, _P(DevOut), _vp]),
     "sdfs_cdc_stream_sync": (ctypes.c_int, [_vp]),
-    "sdfs_cdc_set_pipeline": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint64]),
+    "sdfs_cdc_queue_stats": (ctypes.c_int, [_vp, _u64p, _u64p]),
     "sdfs_cdc_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "sdfs_cdc_set_timing_mask": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32]),
     "sdfs_cdc_kernel_times": (ctypes.c_int, [_vp, _P(ctypes.c_char_p), _P(ctypes.c_float), ctypes.c_int]),

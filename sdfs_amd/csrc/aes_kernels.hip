@@ -774,7 +774,9 @@ int sdfs_cdc_aes_create(int device, const uint8_t* key, uint32_t key_len, sdfs_c
     auto* z = new sdfs_cdc_aes();
     z->device = device;
     z->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    if (const char* v = getenv("SDFS_AES_VARIANT")) z->enc_variant = atoi(v);
+#ifdef SDFS_TUNING
+    if (const char* v = getenv("SDFS_AES_VARIANT")) z->enc_variant = atoi(v);  // A/B (tuning library only)
+#endif
     z->nr = expand_key(key, key_len, z->rk);
     // equivalent inverse cipher: keys in use order, InvMixColumns on the middle rounds
     for (int r = 0; r <= z->nr; r++)

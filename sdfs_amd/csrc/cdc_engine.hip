@@ -1,8 +1,9 @@
 // cdc_engine.hip — host side of the C-ABI (include/sdfs_cdc.h): engine lifecycle, device
-// workspace, the device-resident pipeline, and the host-buffer paths (getChunks / getHash /
-// batched getChunks) with pinned staging.  Drop-in for org.opendedup.hashing.AbstractHashEngine
-// (AbstractHashEngine.java:24-39) as implemented by VariableSha256HashEngine /
-// VariableMD5HashEngine (VariableSha256HashEngine.java:41-121, VariableMD5HashEngine.java:37-108).
+// workspaces, the device-resident pipeline, and the host-buffer paths (getChunks / getHash /
+// batched getChunks) with pinned staging and the coalescing queue for concurrent callers.
+// Drop-in for org.opendedup.hashing.AbstractHashEngine (AbstractHashEngine.java:24-39) as
+// implemented by VariableSha256HashEngine / VariableMD5HashEngine
+// (VariableSha256HashEngine.java:41-121, VariableMD5HashEngine.java:37-108).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -10,16 +11,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <atomic>
-#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/sdfs_cdc.h"
 #include "cdc_internal.h"
+#include "host_queue.h"
 
 using namespace sdfs;
 
@@ -39,7 +38,7 @@ int fail(int code, const char* fmt, ...) {
 
 }  // namespace
 
-// shared with the other C-ABI translation units (dedup_index.hip)
+// shared with the other C-ABI translation units (dedup_index.hip, lz4, aes, map)
 int sdfs::fail_status(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -95,8 +94,9 @@ template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t n = 0;  // elements
+    bool fits(size_t want) const { return p && want <= n; }
     hipError_t ensure(size_t want) {
-        if (want <= n && p) return hipSuccess;
+        if (fits(want)) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
@@ -112,18 +112,54 @@ struct DevBuf {
     }
 };
 
+int pinned_ensure(uint8_t** p, size_t* n, size_t want) {
+    if (*p && *n >= want) return SDFS_CDC_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *n = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(p), std::max<size_t>(want, 64), hipHostMallocDefault) != hipSuccess)
+        return fail(SDFS_CDC_ENOMEM, "hipHostMalloc(%zu) failed", want);
+    *n = std::max<size_t>(want, 64);
+    return SDFS_CDC_OK;
+}
+
 // timed stages (kernel_times order); "pipeline" = device time from the first enqueue to the last
-// kernel of the run on the caller's stream (the stages overlap when the run is sub-batched)
+// kernel of the run on its stream
 constexpr int kNumTimed = 7;
 const char* kKernelNames[kNumTimed] = {"prep", "cdc_scan", "cdc_resolve", "cdc_prefix", "cdc_scatter",
                                        "chunk_hash", "pipeline"};
 enum { K_PREP = 0, K_SCAN, K_RESOLVE, K_PREFIX, K_SCATTER, K_HASH, K_PIPE };
-constexpr int kMaxParts = 16;
-constexpr int kEvPerRun = 2 * (kMaxParts * 5 + 2);
+constexpr int kEvPerRun = 2 * 8;
 
-// One slot of the double-buffered host path (host_batch): pinned staging in and out, the
-// device copy of the packed batch and its output slots.  While the GPU chunks the batch in one
-// slot, the host packs the next batch into the other and unpacks the previous one's results.
+// Device scratch of one pipeline run.  The engine keeps a ring of them so that runs enqueued on
+// different streams (two batches in flight: the coalescing queue, or a caller alternating
+// streams) proceed concurrently on one engine; a workspace is reused only behind the event
+// recorded after its previous run (cross-stream wait, no host sync).
+constexpr uint32_t kSmall = 2 * kMaxBins + 8;  // hist | cursor | overflow, total, wave_ctr ..
+constexpr int kRing = 3;
+
+struct Workspace {
+    DevBuf<uint32_t> bitmap;
+    DevBuf<uint64_t> seg_prefix;
+    DevBuf<uint32_t> small;
+    DevBuf<uint32_t> rec_base;
+    DevBuf<uint32_t> tasks;
+    DevBuf<uint32_t> spec_starts, spec_cnt, spec_next;  // sectioned cut walk of very long buffers
+    DevBuf<uint32_t> x_scratch;  // extent ordering (getHash in bulk): hist | cursor | total, starts | tasks
+    hipEvent_t free_ev = nullptr;
+    bool pending = false;  // free_ev recorded and possibly not reached yet
+    uint32_t* overflow() const { return small.p + 2 * kMaxBins; }
+    void release_all() {
+        for (auto* b : {&bitmap, &small, &rec_base, &tasks, &spec_starts, &spec_cnt, &spec_next, &x_scratch})
+            b->release();
+        seg_prefix.release();
+    }
+};
+
+// One slot of the double-buffered batch path (sdfs_cdc_get_chunks_batch): pinned staging in and
+// out, the device copy of the packed batch and its output slots.  While the GPU chunks the batch
+// in one slot, the host packs the next batch into the other and unpacks the previous one's
+// results.
 struct HostSlot {
     uint8_t* pin_in = nullptr;
     size_t pin_in_n = 0;
@@ -140,108 +176,54 @@ struct HostSlot {
     uint32_t b0 = 0, n = 0, dcap = 0;
 };
 
-// Pageable caller buffers -> pinned staging, split over a small persistent thread pool (the
-// host memcpy, not PCIe, bounds the host path when it runs on one thread).
-struct CopyPiece {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
-};
-
-class CopyPool {
-  public:
-    explicit CopyPool(int workers) {
-        for (int i = 0; i < workers; i++) th_.emplace_back([this] { loop(); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> l(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    void run(const std::vector<CopyPiece>& p) {
-        if (th_.empty() || p.size() < 2) {
-            for (const auto& x : p) memcpy(x.dst, x.src, x.n);
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> l(m_);
-            job_ = &p;
-            next_.store(0);
-            active_ = th_.size();
-            gen_++;
-        }
-        cv_.notify_all();
-        drain(p);  // the calling thread copies too
-        std::unique_lock<std::mutex> l(m_);
-        done_.wait(l, [&] { return active_ == 0; });
-        job_ = nullptr;
-    }
-
-  private:
-    void drain(const std::vector<CopyPiece>& p) {
-        for (size_t i; (i = next_.fetch_add(1)) < p.size();) memcpy(p[i].dst, p[i].src, p[i].n);
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::vector<CopyPiece>* job;
-            {
-                std::unique_lock<std::mutex> l(m_);
-                cv_.wait(l, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                job = job_;
-            }
-            drain(*job);
-            std::lock_guard<std::mutex> l(m_);
-            if (--active_ == 0) done_.notify_all();
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    const std::vector<CopyPiece>* job_ = nullptr;
-    std::atomic<size_t> next_{0};
-    size_t active_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+// Device state of one coalescing-queue slot (host_queue.h): the batch's device copy, its outputs
+// and the pinned result image the callers read:
+//   counts[n] | starts[n*dcap] | lens[n*dcap] | flags[16] | digests[n*dcap*32] | hash digests[nh*32]
+struct QSlotDev {
+    uint8_t* pin_meta = nullptr;  // chunk offs u64[max_reqs] | lens u32 | hash offs u64 | lens u32
+    size_t pin_meta_n = 0;
+    uint8_t* pin_out = nullptr;
+    size_t pin_out_n = 0;
+    DevBuf<uint8_t> data;
+    DevBuf<uint64_t> meta64;  // chunk offs | hash offs
+    DevBuf<uint32_t> meta32;  // chunk lens | hash lens
+    DevBuf<uint32_t> counts, starts, clens, total;
+    DevBuf<uint8_t> digests, h_digests;
+    hipEvent_t done = nullptr;
+    // layout of the batch in flight (read by the callers)
+    uint32_t n = 0, nh = 0, dcap = 0;
+    uint64_t digests_at = 0, hdig_at = 0;
+    std::string err;  // message of a failed launch/wait (set on the queue's threads)
 };
 
 }  // namespace
+
+struct QueueBackend;
 
 struct sdfs_cdc_engine {
     sdfs_cdc_params prm{};
     int degree = 0;
     int num_cus = 256;
-    uint32_t seg_len = 4096;  // bytes of one buffer per lane (multiple of the variant's block)
-    int scan_variant = 0;
+    uint32_t seg_len = 4096;  // bytes of one buffer per scan lane (multiple of the block)
+    int scan_variant = 0;     // 0 = production; others exist only in the tuning build
     int hash_variant = 0;
-    int hash_wg_per_cu = 2;  // persistent hash variant: 256-thread workgroups per CU
+    int hash_wg_per_cu = 2;
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
     uint32_t digest_len = 32;
-    hipStream_t stream = nullptr;
-    std::mutex mu;  // one engine context: calls are serialised (DESIGN.md "Host edge")
+    hipStream_t stream = nullptr;  // direct host paths
+    std::mutex mu;                 // enqueue order of every device operation of the engine
 
     DevBuf<uint8_t> tab_image;
     DevBuf<uint8_t> zero_page;
-    // workspace for run_device
-    DevBuf<uint32_t> bitmap;
-    DevBuf<uint64_t> seg_prefix;
-    DevBuf<uint32_t> small;  // hist[kMaxBins] | cursor[kMaxBins] | overflow[1]
-    DevBuf<uint32_t> rec_base;
-    DevBuf<uint32_t> tasks;
-    DevBuf<uint32_t> spec_starts, spec_cnt, spec_next;  // sectioned cut walk of very long buffers
-    // getHash device buffers and pinned staging
+    Workspace ws[kRing];
+    uint32_t ws_next = 0;
+    // direct getHash device buffers and pinned staging
     DevBuf<uint8_t> h_data;
     DevBuf<uint32_t> o_starts;
     DevBuf<uint8_t> o_digests;
-    DevBuf<uint32_t> x_scratch;  // extent ordering: hist | cursor | total, then starts | tasks
-    DevBuf<uint8_t> x_data;      // host-batch staging of getHash in bulk
+    DevBuf<uint8_t> x_data;  // host-batch staging of getHash in bulk
     DevBuf<uint64_t> x_offs;
     DevBuf<uint32_t> x_lens;
     DevBuf<uint8_t> x_digests;
@@ -252,6 +234,13 @@ struct sdfs_cdc_engine {
     hipStream_t s_h2d = nullptr;
     int copy_threads = 8;
     std::unique_ptr<CopyPool> pool;
+    // coalescing queue for concurrent single-buffer callers
+    hipStream_t qs[2] = {nullptr, nullptr};
+    uint32_t q_next = 0;
+    std::unique_ptr<QueueBackend> qb;
+    std::unique_ptr<CoalescingQueue<QueueBackend>> q;
+    std::mutex q_init;
+    int q_state = 0;  // 0 = not started, 1 = running, -1 = disabled (flag or start failure)
     uint32_t timing_mask = 0xFFFFFFFFu;  // stages timed when timing is on (bit = kKernelNames index)
 
     // per-kernel HIP events for the last `timing_slots` runs (ring); averaged by kernel_times
@@ -263,16 +252,6 @@ struct sdfs_cdc_engine {
     std::vector<TimedRun> ev_runs;
     uint64_t runs_recorded = 0;
     TimedRun* run = nullptr;  // run in flight (nullptr: timing off)
-
-    // sub-batch pipeline: scan of part k+1 on s_scan overlaps resolve..hash of part k on s_post.
-    // Measured NEGATIVE on MI355X (4 GiB step: 1 part 4.84 ms, 2 parts 7.0, 4 parts 9.7, 8 parts
-    // 17.4: the persistent 128 KiB-LDS scan workgroups and the hash workgroups starve each other
-    // in the dispatcher), so the default is 1 part; kept for experiments.
-    int parts = 1;
-    uint64_t part_min_bytes = 512ull << 20;
-    hipStream_t s_scan = nullptr, s_post = nullptr;
-    hipEvent_t ev_in = nullptr, ev_done = nullptr;
-    hipEvent_t ev_scan[kMaxParts] = {};
 };
 
 namespace {
@@ -288,17 +267,7 @@ int validate(const sdfs_cdc_params* p) {
     if (p->min_cmp > SDFS_CDC_MIN_GE) return fail(SDFS_CDC_EINVAL, "bad min_cmp");
     if (p->hash_algo > SDFS_CDC_MD5) return fail(SDFS_CDC_EINVAL, "bad hash_algo");
     if (p->pred_mask >> d) return fail(SDFS_CDC_EINVAL, "pred_mask has bits above the fp degree");
-    return SDFS_CDC_OK;
-}
-
-int pinned_ensure(uint8_t** p, size_t* n, size_t want) {
-    if (*p && *n >= want) return SDFS_CDC_OK;
-    if (*p) (void)hipHostFree(*p);
-    *p = nullptr;
-    *n = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(p), std::max<size_t>(want, 64), hipHostMallocDefault) != hipSuccess)
-        return fail(SDFS_CDC_ENOMEM, "hipHostMalloc(%zu) failed", want);
-    *n = std::max<size_t>(want, 64);
+    if (p->flags & ~(uint32_t)SDFS_CDC_FLAG_DIRECT) return fail(SDFS_CDC_EINVAL, "unknown flags 0x%x", p->flags);
     return SDFS_CDC_OK;
 }
 
@@ -306,6 +275,44 @@ uint32_t slot_cap_for(const sdfs_cdc_params& p, uint64_t len) {
     const uint64_t shortest_cut = p.min_cmp == SDFS_CDC_MIN_GT ? (uint64_t)p.min_len + 1 : std::max<uint64_t>(p.min_len, 1);
     const uint64_t shortest = std::min<uint64_t>(shortest_cut, p.max_len);
     return (uint32_t)(len / shortest + 2);
+}
+
+// ---- workspace ring ----
+struct WsNeed {
+    uint64_t bitmap_words = 0, seg_prefix = 0, rec_base = 0, tasks = 0, spec_starts = 0, spec_items = 0, x_scratch = 0;
+};
+
+// Next workspace of the ring, sized for `nd`, ordered behind its previous use on `s`.  Caller
+// holds e->mu and has set the device.
+int ws_acquire(sdfs_cdc_engine* e, const WsNeed& nd, hipStream_t s, Workspace** out) {
+    Workspace* w = &e->ws[e->ws_next++ % kRing];
+    const bool fits = w->bitmap.fits(nd.bitmap_words) && w->small.fits(kSmall + 8) &&
+                      w->rec_base.fits(nd.rec_base) && w->tasks.fits(nd.tasks) &&
+                      (!nd.seg_prefix || w->seg_prefix.fits(nd.seg_prefix)) &&
+                      (!nd.spec_items || (w->spec_starts.fits(nd.spec_starts) && w->spec_cnt.fits(nd.spec_items) &&
+                                          w->spec_next.fits(nd.spec_items))) &&
+                      (!nd.x_scratch || w->x_scratch.fits(nd.x_scratch));
+    if (!fits && w->pending) HIP_TRY(hipEventSynchronize(w->free_ev));  // never free memory in use
+    HIP_TRY(w->bitmap.ensure(std::max<uint64_t>(nd.bitmap_words, 2)));
+    HIP_TRY(w->small.ensure(kSmall + 8));
+    HIP_TRY(w->rec_base.ensure(std::max<uint64_t>(nd.rec_base, 1)));
+    HIP_TRY(w->tasks.ensure(std::max<uint64_t>(nd.tasks, 1)));
+    if (nd.seg_prefix) HIP_TRY(w->seg_prefix.ensure(nd.seg_prefix));
+    if (nd.spec_items) {
+        HIP_TRY(w->spec_starts.ensure(nd.spec_starts));
+        HIP_TRY(w->spec_cnt.ensure(nd.spec_items));
+        HIP_TRY(w->spec_next.ensure(nd.spec_items));
+    }
+    if (nd.x_scratch) HIP_TRY(w->x_scratch.ensure(nd.x_scratch));
+    if (w->pending) HIP_TRY(hipStreamWaitEvent(s, w->free_ev, 0));
+    *out = w;
+    return SDFS_CDC_OK;
+}
+
+int ws_release(Workspace* w, hipStream_t s) {
+    HIP_TRY(hipEventRecord(w->free_ev, s));
+    w->pending = true;
+    return SDFS_CDC_OK;
 }
 
 // Records a start event for stage `kid` on stream `st` (timing runs only); returns the pair index.
@@ -321,22 +328,34 @@ void t_end(sdfs_cdc_engine* e, int i, hipStream_t st) {
     if (e->run && i >= 0) (void)hipEventRecord(e->run->ev[2 * i + 1], st);
 }
 
-// The device pipeline, enqueued behind everything already on `s` and completing on `s`.  Large
-// uniform batches are split into `parts` sub-batches: the scan of part k+1 (engine stream
-// s_scan) overlaps resolve/prefix/scatter/hash of part k (s_post), so the latency-bound scan and
-// the VALU-bound hash share the CUs (DESIGN.md "Pipeline").  Caller holds e->mu.
-int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
-                 const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
-                 const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len = 0) {
-    if (!out || !out->counts || !out->starts || !out->lens || !out->digests || !out->total)
-        return fail(SDFS_CDC_EINVAL, "incomplete sdfs_cdc_dev_out");
-    if (uniform_len && (uniform_len & 63)) return fail(SDFS_CDC_EINVAL, "uniform_len must be a multiple of 64");
-    if (!uniform_len && (!d_offs || !d_lens)) return fail(SDFS_CDC_EINVAL, "offs/lens required without uniform_len");
-    if ((reinterpret_cast<uintptr_t>(d_data) & 63) != 0) return fail(SDFS_CDC_EINVAL, "d_data must be 64-byte aligned");
-    if (uniform_len) data_bytes = (uint64_t)nbuf * uniform_len;
-    if (uniform_len && out->cap < slot_cap_for(e->prm, uniform_len))
-        return fail(SDFS_CDC_ECAP, "cap %u < slot_cap %u", out->cap, slot_cap_for(e->prm, uniform_len));
+// Workspace needs of one pipeline run.
+WsNeed pipeline_need(const sdfs_cdc_engine* e, uint64_t data_bytes, uint32_t nbuf, uint32_t uniform_len, uint32_t cap,
+                     uint64_t max_buf_len, uint32_t* sec_len_out, uint32_t* nsec_out, uint32_t* spec_cap_out) {
+    WsNeed nd;
+    nd.bitmap_words = ((data_bytes + 63) / 64) * 2 + 2;
+    nd.rec_base = nbuf;
+    nd.tasks = (uint64_t)nbuf * cap;
+    if (!uniform_len) nd.seg_prefix = (uint64_t)nbuf + 1;
+    const uint64_t mbl = uniform_len ? uniform_len : max_buf_len;
+    const uint32_t sec = resolve_section_len(mbl, e->prm.max_len);
+    *sec_len_out = sec;
+    *nsec_out = *spec_cap_out = 0;
+    if (sec) {
+        *nsec_out = (uint32_t)((mbl + sec - 1) / sec);
+        *spec_cap_out = sec / (e->first_off + 1) + 2;
+        nd.spec_items = (uint64_t)nbuf * *nsec_out;
+        nd.spec_starts = nd.spec_items * *spec_cap_out;
+    }
+    return nd;
+}
 
+// The device pipeline (scan [+ fused cut walk] | resolve, prefix, scatter, fingerprint) of one
+// batch, enqueued on `s` behind everything already there, on workspace `w` (acquired by the
+// caller).  Caller holds e->mu.
+int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
+                 const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
+                 const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, uint32_t sec_len, uint32_t nsec,
+                 uint32_t spec_cap) {
     e->run = nullptr;
     if (e->timing_slots > 0) {
         e->run = &e->ev_runs[e->runs_recorded % e->timing_slots];
@@ -345,201 +364,225 @@ int run_pipeline(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
     const int tpipe = t_begin(e, K_PIPE, s);
     if (nbuf == 0) {
         HIP_TRY(hipMemsetAsync(out->total, 0, 4, s));
+        HIP_TRY(hipMemsetAsync(w->small.p, 0, (kSmall + 8) * sizeof(uint32_t), s));
         t_end(e, tpipe, s);
         if (e->run) e->runs_recorded++;
         return SDFS_CDC_OK;
     }
-
-    // sub-batch split (uniform layout only): parts of whole buffers, each >= part_min_bytes
-    uint32_t parts = 1;
-    if (uniform_len && e->parts > 1) {
-        const uint64_t by_size = data_bytes / std::max<uint64_t>(e->part_min_bytes, 1);
-        parts = (uint32_t)std::min<uint64_t>({(uint64_t)e->parts, by_size, (uint64_t)nbuf, (uint64_t)kMaxParts});
-        parts = std::max<uint32_t>(parts, 1);
-    }
-
-    // workspace
-    const uint64_t nwords = ((data_bytes + 63) / 64) * 2 + 2;
-    HIP_TRY(e->bitmap.ensure(nwords));
-    constexpr uint32_t kSmall = 2 * kMaxBins + 8;  // hist | cursor | overflow, total, base_in, base_out ..
-    HIP_TRY(e->small.ensure((uint64_t)kSmall * parts + 8));
-    HIP_TRY(e->rec_base.ensure(nbuf));
-    const uint64_t nslots = (uint64_t)nbuf * out->cap;
-    HIP_TRY(e->tasks.ensure(nslots));
-    uint32_t* running = e->small.p + (uint64_t)kSmall * parts;  // running record base per part
-    hipStream_t sscan = parts > 1 ? e->s_scan : s;
-    hipStream_t spost = parts > 1 ? e->s_post : s;
-    if (parts > 1) {
-        HIP_TRY(hipEventRecord(e->ev_in, s));
-        HIP_TRY(hipStreamWaitEvent(sscan, e->ev_in, 0));
-        HIP_TRY(hipStreamWaitEvent(spost, e->ev_in, 0));
-    }
+    uint32_t* hist = w->small.p;
+    uint32_t* cursor = w->small.p + kMaxBins;
+    uint32_t* total = w->small.p + 2 * kMaxBins + 1;
     {
-        const int t = t_begin(e, K_PREP, spost);
-        HIP_TRY(hipMemsetAsync(e->small.p, 0, ((uint64_t)kSmall * parts + 8) * sizeof(uint32_t), spost));
-        if (!uniform_len) {
-            HIP_TRY(e->seg_prefix.ensure((uint64_t)nbuf + 1));
-            HIP_TRY(launch_seg_prefix(d_lens, nbuf, e->seg_len, e->seg_prefix.p, spost));
-        }
-        t_end(e, t, spost);
+        const int t = t_begin(e, K_PREP, s);
+        HIP_TRY(hipMemsetAsync(w->small.p, 0, (kSmall + 8) * sizeof(uint32_t), s));
+        if (!uniform_len) HIP_TRY(launch_seg_prefix(d_lens, nbuf, e->seg_len, w->seg_prefix.p, s));
+        t_end(e, t, s);
     }
-    if (!uniform_len && sscan != spost) return fail(SDFS_CDC_EINVAL, "internal: ragged batches are not split");
-
     const bool pred64 = (e->prm.pred_mask >> 32) != 0;
-    for (uint32_t p = 0; p < parts; p++) {
-        const uint32_t b0 = (uint32_t)((uint64_t)nbuf * p / parts);
-        const uint32_t b1 = (uint32_t)((uint64_t)nbuf * (p + 1) / parts);
-        const uint32_t nb = b1 - b0;
-        const uint64_t byte0 = uniform_len ? (uint64_t)b0 * uniform_len : 0;
-        const uint8_t* data_p = d_data + byte0;
-        uint32_t* bitmap_p = e->bitmap.p + (byte0 >> 5);
-        uint32_t* small_p = e->small.p + (uint64_t)kSmall * p;
-        uint32_t* hist = small_p;
-        uint32_t* cursor = small_p + kMaxBins;
-        uint32_t* part_total = small_p + 2 * kMaxBins + 1;
-        const uint64_t slot0 = (uint64_t)b0 * out->cap;
-
-        // ---- scan (s_scan)
-        ScanArgs sa{};
-        sa.data = data_p;
-        sa.offs = d_offs;
-        sa.lens = d_lens;
-        sa.bitmap = bitmap_p;
-        sa.nbuf = nb;
-        sa.uniform_len = uniform_len;
-        sa.seg_len = e->seg_len;
-        sa.jshift = (uint32_t)(e->degree - 40);
-        sa.mask_lo = (uint32_t)e->prm.pred_mask;
-        sa.mask_hi = (uint32_t)(e->prm.pred_mask >> 32);
-        sa.val_lo = (uint32_t)e->prm.pred_value;
-        sa.val_hi = (uint32_t)(e->prm.pred_value >> 32);
-        sa.tab_image = e->tab_image.p;
-        sa.zero_page = e->zero_page.p;
-        uint64_t seg_bound;
-        if (uniform_len) {
-            const uint64_t spb = (uniform_len + e->seg_len - 1) / e->seg_len;
-            sa.total_segs = spb * nb;
-            seg_bound = sa.total_segs;
-        } else {
-            sa.seg_prefix = e->seg_prefix.p;
-            seg_bound = data_bytes / e->seg_len + nb;
-        }
-        ResolveArgs ra{};
-        ra.bitmap = bitmap_p;
-        ra.offs = d_offs;
-        ra.lens = d_lens;
-        ra.nbuf = nb;
-        ra.uniform_len = uniform_len;
-        ra.first_off = e->first_off;
-        ra.max_len = e->prm.max_len;
-        ra.cap = out->cap;
-        ra.bin_shift = e->bin_shift;
-        ra.nbins = e->nbins;
-        ra.counts = out->counts + b0;
-        ra.starts = out->starts + slot0;
-        ra.clens = out->lens + slot0;
-        ra.hist = hist;
-        ra.overflow = e->small.p + 2 * kMaxBins;  // part 0's word: one flag for the whole run
-        ra.max_buf_len = uniform_len ? uniform_len : max_buf_len;
-        ra.sec_len = resolve_section_len(ra.max_buf_len, e->prm.max_len);
-        if (ra.sec_len) {
-            ra.nsec = (uint32_t)((ra.max_buf_len + ra.sec_len - 1) / ra.sec_len);
-            ra.spec_cap = ra.sec_len / (e->first_off + 1) + 2;
-            const uint64_t items = (uint64_t)nb * ra.nsec;
-            HIP_TRY(e->spec_starts.ensure(items * ra.spec_cap));
-            HIP_TRY(e->spec_cnt.ensure(items));
-            HIP_TRY(e->spec_next.ensure(items));
-            ra.spec_starts = e->spec_starts.p;
-            ra.spec_cnt = e->spec_cnt.p;
-            ra.spec_next = e->spec_next.p;
-        }
-        // one wave = one buffer: the fused scan variant resolves inside the scan kernel
-        // (single stream only: the histogram it feeds is cleared on the post stream)
-        const bool fused = e->scan_info.fuse && parts == 1 && uniform_len && e->scan_info.chains == 1 &&
-                           (uint64_t)uniform_len == 64ull * e->seg_len && e->seg_len < 0xFFFFu;
-        sa.fuse_resolve = fused ? 1u : 0u;
-        sa.res = ra;
-        const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
-        uint64_t grid = (seg_bound + per_block - 1) / per_block;
-        grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus * e->scan_info.wg_per_cu);
-        grid = std::max<uint64_t>(grid, 1);
-        {
-            const int t = t_begin(e, K_SCAN, sscan);
-            HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, sscan));
-            t_end(e, t, sscan);
-        }
-        if (parts > 1) {
-            HIP_TRY(hipEventRecord(e->ev_scan[p], sscan));
-            HIP_TRY(hipStreamWaitEvent(spost, e->ev_scan[p], 0));
-        }
-
-        // ---- resolve, prefix, scatter, hash (s_post)
-        if (!fused) {
-            const int t = t_begin(e, K_RESOLVE, spost);
-            HIP_TRY(launch_resolve(ra, spost));
-            t_end(e, t, spost);
-        }
-        PrefixArgs pa{};
-        pa.counts = out->counts + b0;
-        pa.nbuf = nb;
-        pa.hist = hist;
-        pa.nbins = e->nbins;
-        pa.cursor = cursor;
-        pa.rec_base = e->rec_base.p + b0;
-        pa.total = part_total;
-        pa.base_in = p ? running + p : nullptr;
-        pa.base_out = running + p + 1;
-        pa.grand_total = p + 1 == parts ? out->total : nullptr;
-        {
-            const int t = t_begin(e, K_PREFIX, spost);
-            HIP_TRY(launch_prefix(pa, spost));
-            t_end(e, t, spost);
-        }
-        ScatterArgs ca{};
-        ca.counts = out->counts + b0;
-        ca.clens = out->lens + slot0;
-        ca.nbuf = nb;
-        ca.cap = out->cap;
-        ca.bin_shift = e->bin_shift;
-        ca.nbins = e->nbins;
-        ca.cursor = cursor;
-        ca.tasks = e->tasks.p + slot0;
-        {
-            const int t = t_begin(e, K_SCATTER, spost);
-            HIP_TRY(launch_scatter(ca, spost));
-            t_end(e, t, spost);
-        }
-        HashArgs ha{};
-    ha.zero_page = e->zero_page.p;
-        ha.data = data_p;
-        ha.offs = d_offs;
-        ha.uniform_len = uniform_len;
-        ha.tasks = e->tasks.p + slot0;
-        ha.total = part_total;
-        ha.starts = out->starts + slot0;
-        ha.clens = out->lens + slot0;
-        ha.rec_base = e->rec_base.p + b0;
-        ha.cap = out->cap;
-        ha.digests = out->digests + slot0 * 32;
-        ha.records = out->records;
-        ha.records_cap = out->records_cap;
-        ha.buffer_id_base = buffer_id_base + b0;
-        ha.algo = e->prm.hash_algo;
-        ha.wave_ctr = small_p + 2 * kMaxBins + 2;  // zeroed with the rest of `small` above
-        ha.persist_grid = (uint32_t)(e->num_cus * e->hash_wg_per_cu);
-        {
-            const int t = t_begin(e, K_HASH, spost);
-            HIP_TRY(launch_hash(ha, (uint64_t)nb * out->cap, e->hash_variant, spost));
-            t_end(e, t, spost);
-        }
+    ScanArgs sa{};
+    sa.data = d_data;
+    sa.offs = d_offs;
+    sa.lens = d_lens;
+    sa.bitmap = w->bitmap.p;
+    sa.nbuf = nbuf;
+    sa.uniform_len = uniform_len;
+    sa.seg_len = e->seg_len;
+    sa.jshift = (uint32_t)(e->degree - 40);
+    sa.mask_lo = (uint32_t)e->prm.pred_mask;
+    sa.mask_hi = (uint32_t)(e->prm.pred_mask >> 32);
+    sa.val_lo = (uint32_t)e->prm.pred_value;
+    sa.val_hi = (uint32_t)(e->prm.pred_value >> 32);
+    sa.tab_image = e->tab_image.p;
+    sa.zero_page = e->zero_page.p;
+    uint64_t seg_bound;
+    if (uniform_len) {
+        const uint64_t spb = (uniform_len + e->seg_len - 1) / e->seg_len;
+        sa.total_segs = spb * nbuf;
+        seg_bound = sa.total_segs;
+    } else {
+        sa.seg_prefix = w->seg_prefix.p;
+        seg_bound = data_bytes / e->seg_len + nbuf;
     }
-    if (parts > 1) {
-        HIP_TRY(hipEventRecord(e->ev_done, spost));
-        HIP_TRY(hipStreamWaitEvent(s, e->ev_done, 0));
+    ResolveArgs ra{};
+    ra.bitmap = w->bitmap.p;
+    ra.offs = d_offs;
+    ra.lens = d_lens;
+    ra.nbuf = nbuf;
+    ra.uniform_len = uniform_len;
+    ra.first_off = e->first_off;
+    ra.max_len = e->prm.max_len;
+    ra.cap = out->cap;
+    ra.bin_shift = e->bin_shift;
+    ra.nbins = e->nbins;
+    ra.counts = out->counts;
+    ra.starts = out->starts;
+    ra.clens = out->lens;
+    ra.hist = hist;
+    ra.overflow = w->overflow();
+    ra.max_buf_len = uniform_len ? uniform_len : max_buf_len;
+    ra.sec_len = sec_len;
+    if (sec_len) {
+        ra.nsec = nsec;
+        ra.spec_cap = spec_cap;
+        ra.spec_starts = w->spec_starts.p;
+        ra.spec_cnt = w->spec_cnt.p;
+        ra.spec_next = w->spec_next.p;
+    }
+    // one wave = one buffer: the scan kernel resolves the cuts in its epilogue
+    const bool fused = e->scan_info.fuse && uniform_len && e->scan_info.chains == 1 &&
+                       (uint64_t)uniform_len == 64ull * e->seg_len && e->seg_len < 0xFFFFu;
+    sa.fuse_resolve = fused ? 1u : 0u;
+    sa.res = ra;
+    const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
+    uint64_t grid = (seg_bound + per_block - 1) / per_block;
+    grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus * e->scan_info.wg_per_cu);
+    grid = std::max<uint64_t>(grid, 1);
+    {
+        const int t = t_begin(e, K_SCAN, s);
+        HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, s));
+        t_end(e, t, s);
+    }
+    if (!fused) {
+        const int t = t_begin(e, K_RESOLVE, s);
+        HIP_TRY(launch_resolve(ra, s));
+        t_end(e, t, s);
+    }
+    PrefixArgs pa{};
+    pa.counts = out->counts;
+    pa.nbuf = nbuf;
+    pa.hist = hist;
+    pa.nbins = e->nbins;
+    pa.cursor = cursor;
+    pa.rec_base = w->rec_base.p;
+    pa.total = total;
+    pa.grand_total = out->total;
+    {
+        const int t = t_begin(e, K_PREFIX, s);
+        HIP_TRY(launch_prefix(pa, s));
+        t_end(e, t, s);
+    }
+    ScatterArgs ca{};
+    ca.counts = out->counts;
+    ca.clens = out->lens;
+    ca.nbuf = nbuf;
+    ca.cap = out->cap;
+    ca.bin_shift = e->bin_shift;
+    ca.nbins = e->nbins;
+    ca.cursor = cursor;
+    ca.tasks = w->tasks.p;
+    {
+        const int t = t_begin(e, K_SCATTER, s);
+        HIP_TRY(launch_scatter(ca, s));
+        t_end(e, t, s);
+    }
+    HashArgs ha{};
+    ha.zero_page = e->zero_page.p;
+    ha.data = d_data;
+    ha.offs = d_offs;
+    ha.uniform_len = uniform_len;
+    ha.tasks = w->tasks.p;
+    ha.total = total;
+    ha.starts = out->starts;
+    ha.clens = out->lens;
+    ha.rec_base = w->rec_base.p;
+    ha.cap = out->cap;
+    ha.digests = out->digests;
+    ha.records = out->records;
+    ha.records_cap = out->records_cap;
+    ha.buffer_id_base = buffer_id_base;
+    ha.algo = e->prm.hash_algo;
+    ha.wave_ctr = w->small.p + 2 * kMaxBins + 2;  // zeroed with the rest of `small` above
+    ha.persist_grid = (uint32_t)(e->num_cus * e->hash_wg_per_cu);
+    {
+        const int t = t_begin(e, K_HASH, s);
+        HIP_TRY(launch_hash(ha, (uint64_t)nbuf * out->cap, e->hash_variant, s));
+        t_end(e, t, s);
     }
     t_end(e, tpipe, s);
     if (e->run) e->runs_recorded++;
     return SDFS_CDC_OK;
+}
+
+// Validates a device-run request, acquires a workspace and runs the pipeline on `s`.  The
+// overflow flag of the run is left at *ovf_dev (device word, valid until the workspace's next
+// use) when ovf_dev != NULL.  Caller holds e->mu.
+int device_run(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
+               const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
+               const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, const uint32_t** ovf_dev) {
+    if (!out || !out->counts || !out->starts || !out->lens || !out->digests || !out->total)
+        return fail(SDFS_CDC_EINVAL, "incomplete sdfs_cdc_dev_out");
+    if (uniform_len && (uniform_len & 63)) return fail(SDFS_CDC_EINVAL, "uniform_len must be a multiple of 64");
+    if (!uniform_len && nbuf && (!d_offs || !d_lens)) return fail(SDFS_CDC_EINVAL, "offs/lens required without uniform_len");
+    if ((reinterpret_cast<uintptr_t>(d_data) & 63) != 0) return fail(SDFS_CDC_EINVAL, "d_data must be 64-byte aligned");
+    if (uniform_len) data_bytes = (uint64_t)nbuf * uniform_len;
+    if (uniform_len && out->cap < slot_cap_for(e->prm, uniform_len))
+        return fail(SDFS_CDC_ECAP, "cap %u < slot_cap %u", out->cap, slot_cap_for(e->prm, uniform_len));
+    uint32_t sec_len, nsec, spec_cap;
+    const WsNeed nd = pipeline_need(e, data_bytes, nbuf, uniform_len, out->cap, max_buf_len, &sec_len, &nsec, &spec_cap);
+    Workspace* w = nullptr;
+    int rc = ws_acquire(e, nd, s, &w);
+    if (rc) return rc;
+    rc = run_pipeline(e, w, d_data, data_bytes, d_offs, d_lens, nbuf, uniform_len, buffer_id_base, out, s, max_buf_len,
+                      sec_len, nsec, spec_cap);
+    const int rr = ws_release(w, s);  // even after a failed enqueue: what was enqueued completes first
+    if (ovf_dev) *ovf_dev = w->overflow();
+    return rc ? rc : rr;
+}
+
+// Fingerprints of n extents on workspace scratch (getHash in bulk).  Caller holds e->mu.
+int hash_extents(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
+                 const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, hipStream_t s) {
+    if (n_max == 0) return SDFS_CDC_OK;
+    if (n_max > 0xFFFFFFFFull) return fail(SDFS_CDC_EINVAL, "more than 2^32 extents");
+    WsNeed nd;
+    nd.x_scratch = kExtentScratchWords + 2 * n_max;
+    Workspace* w = nullptr;
+    int rc = ws_acquire(e, nd, s, &w);
+    if (rc) return rc;
+    uint32_t* sc = w->x_scratch.p;
+    ExtentArgs xa{d_lens, d_count, n_max, sc + kExtentScratchWords, sc + kExtentScratchWords + n_max,
+                  sc + 1024, sc, sc + 512};
+    hipError_t he = launch_extent_order(xa, s);
+    if (he == hipSuccess) {
+        HashArgs ha{};
+        ha.zero_page = e->zero_page.p;
+        ha.data = d_data;
+        ha.offs = d_offs;
+        ha.uniform_len = 0;
+        ha.tasks = xa.tasks;
+        ha.total = xa.total;
+        ha.starts = xa.starts;
+        ha.clens = d_lens;
+        ha.cap = 1;
+        ha.digests = d_digests;
+        ha.algo = e->prm.hash_algo;
+        he = launch_hash(ha, n_max, 0, s);
+    }
+    const int rr = ws_release(w, s);
+    if (he != hipSuccess) return fail(SDFS_CDC_EHIP, "extent hashing: %s", hipGetErrorString(he));
+    return rr;
+}
+
+// ---- host batch path (sdfs_cdc_get_chunks_batch) ----
+
+// True when [p, p+n) lies inside ONE page-locked host allocation (hipHostMalloc or
+// hipHostRegister), so the H2D copy may read it in place.
+bool host_range_pinned(const uint8_t* p, uint64_t n) {
+    if (!n) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost) {
+        (void)hipGetLastError();  // pageable memory reports an error here: clear it
+        return false;
+    }
+    void* start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const uint8_t* s = static_cast<const uint8_t*>(start);
+    return s <= p && p + n <= s + size;
 }
 
 // Results of the batch in slot `sl` (synchronises on it) -> the caller's arrays.
@@ -583,20 +626,12 @@ int host_batch_impl(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* off
     hipStream_t s = e->stream;
     std::vector<CopyPiece> pieces;
     uint32_t b0 = 0, k = 0;
-    // is the caller's input pinned host memory (both ends of the span)?
-    bool host_pinned = false;
-    {
-        uint64_t lo = UINT64_MAX, hi = 0;
-        for (uint32_t i = 0; i < nbuf; i++) {
-            lo = std::min<uint64_t>(lo, offs[i]);
-            hi = std::max<uint64_t>(hi, offs[i] + lens[i]);
-        }
-        hipPointerAttribute_t a0, a1;
-        if (hi > lo && hipPointerGetAttributes(&a0, base + lo) == hipSuccess &&
-            hipPointerGetAttributes(&a1, base + hi - 1) == hipSuccess)
-            host_pinned = a0.type == hipMemoryTypeHost && a1.type == hipMemoryTypeHost;
-        (void)hipGetLastError();  // pageable memory reports an error here: clear it
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < nbuf; i++) {
+        lo = std::min<uint64_t>(lo, offs[i]);
+        hi = std::max<uint64_t>(hi, offs[i] + lens[i]);
     }
+    const bool host_pinned = hi > lo && host_range_pinned(base + lo, hi - lo);
     while (b0 < nbuf) {
         HostSlot& sl = e->hs[k++ & 1];
         if (sl.busy) {
@@ -615,8 +650,8 @@ int host_batch_impl(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* off
         }
         const uint32_t n = b1 - b0;
         const uint32_t dcap = slot_cap_for(e->prm, maxlen);
-        // Pinned (hipHostMalloc'd or hipHostRegister'ed) input whose buffers sit back to back at
-        // 64-byte multiples: copy it to the GPU straight from the caller's memory (no staging).
+        // Pinned input whose buffers sit back to back at 64-byte multiples: copy it to the GPU
+        // straight from the caller's memory (no staging).
         bool direct = host_pinned;
         for (uint32_t i = 0; direct && i < n; i++)
             direct = (lens[b0 + i] & 63u) == 0 && (i == 0 || offs[b0 + i] == offs[b0 + i - 1] + lens[b0 + i - 1]);
@@ -665,7 +700,8 @@ int host_batch_impl(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* off
         out.digests = sl.digests.p;
         out.cap = dcap;
         out.total = sl.total.p;
-        rc = run_pipeline(e, sl.data.p, bytes, sl.offs.p, sl.lens.p, n, 0, 0, &out, s, maxlen);
+        const uint32_t* ovf = nullptr;
+        rc = device_run(e, sl.data.p, bytes, sl.offs.p, sl.lens.p, n, 0, 0, &out, s, maxlen, &ovf);
         if (rc) return rc;
         // results back through pinned memory: counts | starts | lens | overflow flag (64 B) | digests
         uint32_t* pc = reinterpret_cast<uint32_t*>(sl.pin_out);
@@ -676,8 +712,7 @@ int host_batch_impl(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* off
         HIP_TRY(hipMemcpyAsync(pc, out.counts, n * 4ull, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(ps, out.starts, nout * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(pl, out.lens, nout * 4, hipMemcpyDeviceToHost, s));
-        // the run-wide overflow flag, read before the next batch's pipeline clears it
-        HIP_TRY(hipMemcpyAsync(povf, e->small.p + 2 * kMaxBins, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(povf, ovf, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(pd, out.digests, nout * 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipEventRecord(sl.done, s));
         sl.busy = true;
@@ -705,6 +740,226 @@ int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, co
         (void)hipStreamSynchronize(e->s_h2d);
         (void)hipStreamSynchronize(e->stream);
         e->hs[0].busy = e->hs[1].busy = false;
+    }
+    return rc;
+}
+
+// Direct getHash (inputs larger than a queue slot, or the queue disabled).  Caller holds e->mu.
+int get_hash_direct(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest) {
+    hipStream_t s = e->stream;
+    int rc = pinned_ensure(&e->pin_data, &e->pin_data_n, len + 256);
+    if (rc) return rc;
+    if (len) memcpy(e->pin_data, data, len);
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(e->pin_data + ((len + 63) & ~63ull));
+    ctl[0] = 0;                  // starts[0]
+    ctl[1] = (uint32_t)len;      // lens[0]
+    ctl[2] = 0;                  // tasks[0]
+    ctl[3] = 1;                  // total
+    HIP_TRY(e->h_data.ensure(std::max<uint64_t>(len, 64) + 64));
+    HIP_TRY(e->o_starts.ensure(4));
+    HIP_TRY(e->o_digests.ensure(32));
+    if (len) HIP_TRY(hipMemcpyAsync(e->h_data.p, e->pin_data, len, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->o_starts.p, ctl, 16, hipMemcpyHostToDevice, s));
+    HashArgs ha{};
+    ha.zero_page = e->zero_page.p;
+    ha.data = e->h_data.p;
+    ha.uniform_len = 64;  // buffer 0 at offset 0
+    ha.starts = e->o_starts.p;
+    ha.clens = e->o_starts.p + 1;
+    ha.tasks = e->o_starts.p + 2;
+    ha.total = e->o_starts.p + 3;
+    ha.cap = 1;
+    ha.digests = e->o_digests.p;
+    ha.algo = e->prm.hash_algo;
+    HIP_TRY(launch_hash(ha, 1, 0, s));
+    HIP_TRY(hipMemcpyAsync(ctl + 4, e->o_digests.p, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    memcpy(digest, ctl + 4, e->digest_len);
+    return SDFS_CDC_OK;
+}
+
+}  // namespace
+
+// ---- coalescing-queue backend (host_queue.h) ----
+struct QueueBackend {
+    sdfs_cdc_engine* e;
+    uint64_t slot_bytes;
+    uint32_t max_reqs;
+
+    int prepare(QSlot& s) {
+        HIP_TRY(hipSetDevice(e->prm.device));
+        auto* d = new QSlotDev();
+        s.dev = d;
+        int rc = pinned_ensure(&s.in, &s.cap, slot_bytes);
+        if (!rc) rc = pinned_ensure(&d->pin_meta, &d->pin_meta_n, (size_t)max_reqs * 24 + 64);
+        if (rc) return rc;
+        s.cap = slot_bytes;
+        HIP_TRY(d->data.ensure(slot_bytes));
+        HIP_TRY(d->meta64.ensure(2ull * max_reqs));
+        HIP_TRY(d->meta32.ensure(2ull * max_reqs));
+        HIP_TRY(d->total.ensure(1));
+        HIP_TRY(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
+        return SDFS_CDC_OK;
+    }
+
+    void release(QSlot& s) {
+        auto* d = static_cast<QSlotDev*>(s.dev);
+        (void)hipSetDevice(e->prm.device);
+        if (d) {
+            if (d->done) {
+                (void)hipEventSynchronize(d->done);
+                (void)hipEventDestroy(d->done);
+            }
+            if (d->pin_meta) (void)hipHostFree(d->pin_meta);
+            if (d->pin_out) (void)hipHostFree(d->pin_out);
+            for (auto* b : {&d->counts, &d->starts, &d->clens, &d->total, &d->meta32}) b->release();
+            d->meta64.release();
+            d->data.release();
+            d->digests.release();
+            d->h_digests.release();
+            delete d;
+        }
+        if (s.in) (void)hipHostFree(s.in);
+        s.in = nullptr;
+        s.cap = 0;
+        s.dev = nullptr;
+    }
+
+    // Runs on the queue's dispatcher thread: the error message goes with the slot to the callers.
+    int launch(QSlot& s) {
+        std::lock_guard<std::mutex> lk(e->mu);
+        auto* d = static_cast<QSlotDev*>(s.dev);
+        d->err.clear();
+        hipStream_t st = e->qs[e->q_next++ & 1];
+        const int rc = launch_impl(s, d, st);
+        if (rc) {
+            d->err = g_last_error;
+            (void)hipStreamSynchronize(st);  // nothing of a failed batch stays in flight
+        }
+        return rc;
+    }
+
+    // H2D of the slot's bytes and metadata, the CDC pipeline over its getChunks buffers, the
+    // fingerprints of its getHash extents, D2H of the result image; all on one of the engine's
+    // two queue streams (two batches in flight overlap on the device).  Caller holds e->mu.
+    int launch_impl(QSlot& s, QSlotDev* d, hipStream_t st) {
+        HIP_TRY(hipSetDevice(e->prm.device));
+        const uint32_t n = (uint32_t)s.chunks.size(), nh = (uint32_t)s.hashes.size();
+        const uint32_t dcap = n ? slot_cap_for(e->prm, std::max<uint64_t>(s.max_chunk_len, 1)) : 0;
+        const uint64_t nout = (uint64_t)n * dcap;
+        d->n = n;
+        d->nh = nh;
+        d->dcap = dcap;
+        d->digests_at = (n * 4ull + nout * 8 + 64 + 15) & ~15ull;
+        d->hdig_at = d->digests_at + nout * 32;
+        int rc = pinned_ensure(&d->pin_out, &d->pin_out_n, d->hdig_at + nh * 32ull + 64);
+        if (rc) return rc;
+        uint64_t* m64 = reinterpret_cast<uint64_t*>(d->pin_meta);
+        uint32_t* m32 = reinterpret_cast<uint32_t*>(m64 + 2ull * max_reqs);
+        for (uint32_t i = 0; i < n; i++) {
+            m64[i] = s.chunks[i]->off;
+            m32[i] = (uint32_t)s.chunks[i]->len;
+        }
+        for (uint32_t j = 0; j < nh; j++) {
+            m64[max_reqs + j] = s.hashes[j]->off;
+            m32[max_reqs + j] = (uint32_t)s.hashes[j]->len;
+        }
+        if (s.lo) HIP_TRY(hipMemcpyAsync(d->data.p, s.in, s.lo, hipMemcpyHostToDevice, st));
+        if (s.hi < s.cap) HIP_TRY(hipMemcpyAsync(d->data.p + s.hi, s.in + s.hi, s.cap - s.hi, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d->meta64.p, m64, 16ull * max_reqs, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d->meta32.p, m32, 8ull * max_reqs, hipMemcpyHostToDevice, st));
+        uint32_t* pc = reinterpret_cast<uint32_t*>(d->pin_out);
+        uint32_t* ps = pc + n;
+        uint32_t* pl = ps + nout;
+        uint32_t* pflag = pl + nout;
+        pflag[0] = 0;
+        if (n) {
+            HIP_TRY(d->counts.ensure(n));
+            HIP_TRY(d->starts.ensure(nout));
+            HIP_TRY(d->clens.ensure(nout));
+            HIP_TRY(d->digests.ensure(nout * 32));
+            sdfs_cdc_dev_out out{};
+            out.counts = d->counts.p;
+            out.starts = d->starts.p;
+            out.lens = d->clens.p;
+            out.digests = d->digests.p;
+            out.cap = dcap;
+            out.total = d->total.p;
+            // every CHUNK_LENGTH flush buffer (the common case) takes the uniform layout and the
+            // fused cut walk; mixed lengths (write-accelerator runs) the ragged one
+            const uint32_t ul = (s.uniform_len && (s.uniform_len & 63) == 0) ? s.uniform_len : 0;
+            const uint32_t* ovf = nullptr;
+            rc = device_run(e, d->data.p, s.lo, ul ? nullptr : d->meta64.p, ul ? nullptr : d->meta32.p, n, ul, 0,
+                            &out, st, s.max_chunk_len, &ovf);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(pc, out.counts, n * 4ull, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(ps, out.starts, nout * 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(pl, out.lens, nout * 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(pflag, ovf, 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(d->pin_out + d->digests_at, out.digests, nout * 32, hipMemcpyDeviceToHost, st));
+        }
+        if (nh) {
+            HIP_TRY(d->h_digests.ensure(32ull * nh));
+            rc = hash_extents(e, d->data.p, d->meta64.p + max_reqs, d->meta32.p + max_reqs, nullptr, nh,
+                              d->h_digests.p, st);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(d->pin_out + d->hdig_at, d->h_digests.p, 32ull * nh, hipMemcpyDeviceToHost, st));
+        }
+        HIP_TRY(hipEventRecord(d->done, st));
+        return SDFS_CDC_OK;
+    }
+
+    // Runs on the queue's completer thread.
+    int wait(QSlot& s) {
+        auto* d = static_cast<QSlotDev*>(s.dev);
+        const int rc = wait_impl(d);
+        if (rc && d->err.empty()) d->err = g_last_error;
+        return rc;
+    }
+
+    int wait_impl(QSlotDev* d) {
+        HIP_TRY(hipSetDevice(e->prm.device));
+        HIP_TRY(hipEventSynchronize(d->done));
+        if (d->n) {
+            const uint32_t* pflag = reinterpret_cast<const uint32_t*>(d->pin_out) + d->n + 2ull * d->n * d->dcap;
+            if (*pflag) return fail(SDFS_CDC_EHIP, "internal: chunk slot overflow");
+        }
+        return SDFS_CDC_OK;
+    }
+};
+
+namespace {
+
+// Starts the queue on first use (slot staging: 4 x CHUNK_LENGTH, at least 64 MiB, at most 512 MiB).
+bool queue_ready(sdfs_cdc_engine* e) {
+    std::lock_guard<std::mutex> lk(e->q_init);
+    if (e->q_state) return e->q_state > 0;
+    const uint64_t slot = std::min<uint64_t>(std::max<uint64_t>(64ull << 20, 4ull * e->prm.chunk_length), 512ull << 20);
+    e->qb.reset(new QueueBackend{e, slot, 1024});
+    CoalescingQueue<QueueBackend>::Config c;
+    c.nslots = 4;
+    c.max_inflight = 2;
+    c.max_reqs = 1024;
+    c.max_req_bytes = slot / 2;
+    e->q.reset(new CoalescingQueue<QueueBackend>(*e->qb, c));
+    if (e->q->start() != 0) {  // pinned/device allocation failed: the direct path serves every call
+        e->q.reset();
+        e->qb.reset();
+        e->q_state = -1;
+        return false;
+    }
+    e->q_state = 1;
+    return true;
+}
+
+// A queued call's outcome: the batch's failure (its message becomes this thread's last error),
+// a queue-level refusal, or the caller's own status.
+int queue_result(int rc, const QSlot* s) {
+    if (rc == kQueueStopped) return fail(SDFS_CDC_EINVAL, "engine is shutting down");
+    if (rc == kQueueTooBig) return fail(SDFS_CDC_EINVAL, "request larger than a queue slot");
+    if (rc && s && s->dev) {
+        const auto* d = static_cast<const QSlotDev*>(s->dev);
+        g_last_error = d->err.empty() ? "batch failed" : d->err;
     }
     return rc;
 }
@@ -753,36 +1008,32 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     e->first_off = p->min_cmp == SDFS_CDC_MIN_GT ? p->min_len : (p->min_len ? p->min_len - 1 : 0);
     e->digest_len = p->hash_algo == SDFS_CDC_SHA256 ? 32 : (p->hash_algo == SDFS_CDC_SHA256_160 ? 20 : 16);
+    if (p->flags & SDFS_CDC_FLAG_DIRECT) e->q_state = -1;
     // bins over SHA block counts: maxLen chunk = (max_len + 8)/64 + 1 blocks
     const uint32_t maxblocks = (p->max_len + 8) / 64 + 1;
     e->bin_shift = 0;
     while ((maxblocks >> e->bin_shift) >= (uint32_t)kMaxBins) e->bin_shift++;
     e->nbins = (maxblocks >> e->bin_shift) + 1;
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->s_scan, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->s_post, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_done, hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&e->hs[0].h2d, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->hs[0].done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->hs[1].h2d, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->hs[1].done, hipEventDisableTiming) != hipSuccess) {
+    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->qs[0], hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->qs[1], hipStreamNonBlocking) == hipSuccess;
+    for (auto& sl : e->hs)
+        ok = ok && hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
+    for (auto& w : e->ws) ok = ok && hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         sdfs_cdc_destroy(e);
         return fail(SDFS_CDC_EHIP, "stream/event creation failed");
     }
+#ifdef SDFS_TUNING
+    // measurement-only overrides (tuning library; the product library reads no environment)
     if (const char* v = getenv("SDFS_COPY_THREADS")) e->copy_threads = std::max(1, std::min(atoi(v), 64));
-    for (auto& ev : e->ev_scan)
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-            sdfs_cdc_destroy(e);
-            return fail(SDFS_CDC_EHIP, "event creation failed");
-        }
-    if (const char* v = getenv("SDFS_PIPE_PARTS")) e->parts = std::max(1, std::min(atoi(v), kMaxParts));
-    // tuning overrides for experiments (DESIGN.md "Scan variants"); production uses variant 0
     if (const char* v = getenv("SDFS_SCAN_VARIANT")) e->scan_variant = atoi(v);
     if (const char* v = getenv("SDFS_SEG_LEN")) e->seg_len = (uint32_t)atoi(v);
     if (const char* v = getenv("SDFS_HASH_VARIANT")) e->hash_variant = atoi(v);
     if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
+#endif
     e->scan_info = scan_variant_info(e->scan_variant);
     if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0) {
         sdfs_cdc_destroy(e);
@@ -801,30 +1052,28 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
 
 int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
     if (!e) return SDFS_CDC_OK;
+    if (e->q) e->q->shutdown();  // joins the queue threads (no call may be in progress)
+    e->q.reset();
+    e->qb.reset();
     {
         std::lock_guard<std::mutex> lk(e->mu);
         (void)hipSetDevice(e->prm.device);
-        if (e->stream) (void)hipStreamSynchronize(e->stream);
+        for (hipStream_t s : {e->stream, e->s_h2d, e->qs[0], e->qs[1]})
+            if (s) (void)hipStreamSynchronize(s);
         e->tab_image.release();
         e->zero_page.release();
-        e->bitmap.release();
-        e->seg_prefix.release();
-        e->small.release();
-        e->rec_base.release();
-        e->tasks.release();
-        e->spec_starts.release();
-        e->spec_cnt.release();
-        e->spec_next.release();
+        for (auto& w : e->ws) {
+            w.release_all();
+            if (w.free_ev) (void)hipEventDestroy(w.free_ev);
+        }
         e->h_data.release();
         e->o_starts.release();
         e->o_digests.release();
-        e->x_scratch.release();
         e->x_data.release();
         e->x_offs.release();
         e->x_lens.release();
         e->x_digests.release();
         if (e->pin_data) (void)hipHostFree(e->pin_data);
-        if (e->s_h2d) (void)hipStreamSynchronize(e->s_h2d);
         for (auto& sl : e->hs) {
             if (sl.pin_in) (void)hipHostFree(sl.pin_in);
             if (sl.pin_out) (void)hipHostFree(sl.pin_out);
@@ -837,19 +1086,11 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
             if (sl.done) (void)hipEventDestroy(sl.done);
         }
         e->pool.reset();
-        if (e->s_scan) (void)hipStreamSynchronize(e->s_scan);
-        if (e->s_post) (void)hipStreamSynchronize(e->s_post);
         for (auto& run : e->ev_runs)
             for (auto& ev : run.ev)
                 if (ev) (void)hipEventDestroy(ev);
-        for (auto& ev : e->ev_scan)
-            if (ev) (void)hipEventDestroy(ev);
-        if (e->ev_in) (void)hipEventDestroy(e->ev_in);
-        if (e->ev_done) (void)hipEventDestroy(e->ev_done);
-        if (e->stream) (void)hipStreamDestroy(e->stream);
-        if (e->s_scan) (void)hipStreamDestroy(e->s_scan);
-        if (e->s_post) (void)hipStreamDestroy(e->s_post);
-        if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
+        for (hipStream_t s : {e->stream, e->s_h2d, e->qs[0], e->qs[1]})
+            if (s) (void)hipStreamDestroy(s);
     }
     delete e;
     return SDFS_CDC_OK;
@@ -868,10 +1109,12 @@ int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_
     if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
     if (!uniform_len)
         return fail(SDFS_CDC_EINVAL, "sdfs_cdc_run_device: ragged layouts need sdfs_cdc_run_device_ragged");
+    (void)d_offs;
+    (void)d_lens;
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-    return run_pipeline(e, d_data, 0, d_offs, d_lens, nbuf, uniform_len, buffer_id_base, out, s);
+    return device_run(e, d_data, 0, nullptr, nullptr, nbuf, uniform_len, buffer_id_base, out, s, 0, nullptr);
 }
 
 int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
@@ -884,7 +1127,7 @@ int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64
     // the longest buffer is not known on the host: a few buffers sharing data_bytes are treated as
     // long (LDS-staged cut walk), many as their mean length
     const uint64_t max_len_hint = nbuf <= 4u * (uint32_t)e->num_cus ? data_bytes : data_bytes / (nbuf ? nbuf : 1);
-    return run_pipeline(e, d_data, data_bytes, d_offs, d_lens, nbuf, 0, buffer_id_base, out, s, max_len_hint);
+    return device_run(e, d_data, data_bytes, d_offs, d_lens, nbuf, 0, buffer_id_base, out, s, max_len_hint, nullptr);
 }
 
 int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns) { return sdfs_cdc_set_timing_mask(e, nruns, 0xFFFFFFFFu); }
@@ -930,15 +1173,6 @@ int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int
     return k;
 }
 
-int sdfs_cdc_set_pipeline(sdfs_cdc_engine* e, int parts, uint64_t part_min_bytes) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    if (parts < 1 || parts > kMaxParts) return fail(SDFS_CDC_EINVAL, "parts %d outside [1,%d]", parts, kMaxParts);
-    std::lock_guard<std::mutex> lk(e->mu);
-    e->parts = parts;
-    e->part_min_bytes = part_min_bytes;
-    return SDFS_CDC_OK;
-}
-
 int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
                               uint32_t nbuf, uint32_t* counts, uint32_t* starts, uint32_t* lens_out,
                               uint8_t* digests, uint32_t cap) {
@@ -955,7 +1189,31 @@ int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, ui
     if (!e || !count) return fail(SDFS_CDC_EINVAL, "null argument");
     *count = 0;
     if (len == 0) return SDFS_CDC_OK;  // an empty byte[] yields no Finger
-    if (!buf) return fail(SDFS_CDC_EINVAL, "null buffer");
+    if (!buf || !starts || !lens) return fail(SDFS_CDC_EINVAL, "null buffer");
+    if (queue_ready(e) && e->q->accepts(len)) {
+        QReq r;
+        r.kind = QReq::kChunks;
+        r.src = buf;
+        r.len = len;
+        const uint32_t dl = e->digest_len;
+        const int rc = e->q->run(r, [&](const QSlot& s, const QReq& q, int status) -> int {
+            if (status) return queue_result(status, &s);
+            const auto* d = static_cast<const QSlotDev*>(s.dev);
+            const uint32_t* pc = reinterpret_cast<const uint32_t*>(d->pin_out);
+            const uint32_t c = pc[q.idx];
+            if (c > cap) return fail(SDFS_CDC_ECAP, "buffer has %u chunks > cap %u", c, cap);
+            const uint64_t so = (uint64_t)q.idx * d->dcap, nout = (uint64_t)d->n * d->dcap;
+            memcpy(starts, pc + d->n + so, c * 4ull);
+            memcpy(lens, pc + d->n + nout + so, c * 4ull);
+            if (digests) {
+                const uint8_t* pd = d->pin_out + d->digests_at + so * 32;
+                for (uint32_t k = 0; k < c; k++) memcpy(digests + (uint64_t)k * dl, pd + k * 32ull, dl);
+            }
+            *count = c;
+            return SDFS_CDC_OK;
+        });
+        return rc == kQueueStopped || rc == kQueueTooBig ? queue_result(rc, nullptr) : rc;
+    }
     const uint64_t off = 0;
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
@@ -965,67 +1223,32 @@ int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, ui
 int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest) {
     if (!e || !digest || (len && !data)) return fail(SDFS_CDC_EINVAL, "null argument");
     if (len > 0xFFFFFFFFull) return fail(SDFS_CDC_EINVAL, "getHash input > 4 GiB");
+    if (queue_ready(e) && e->q->accepts(len)) {
+        QReq r;
+        r.kind = QReq::kHash;
+        r.src = data;
+        r.len = len;
+        const uint32_t dl = e->digest_len;
+        const int rc = e->q->run(r, [&](const QSlot& s, const QReq& q, int status) -> int {
+            if (status) return queue_result(status, &s);
+            const auto* d = static_cast<const QSlotDev*>(s.dev);
+            memcpy(digest, d->pin_out + d->hdig_at + 32ull * q.idx, dl);
+            return SDFS_CDC_OK;
+        });
+        return rc == kQueueStopped || rc == kQueueTooBig ? queue_result(rc, nullptr) : rc;
+    }
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
-    hipStream_t s = e->stream;
-    int rc = pinned_ensure(&e->pin_data, &e->pin_data_n, len + 256);
-    if (rc) return rc;
-    if (len) memcpy(e->pin_data, data, len);
-    uint32_t* ctl = reinterpret_cast<uint32_t*>(e->pin_data + ((len + 63) & ~63ull));
-    ctl[0] = 0;                  // starts[0]
-    ctl[1] = (uint32_t)len;      // lens[0]
-    ctl[2] = 0;                  // tasks[0]
-    ctl[3] = 1;                  // total
-    HIP_TRY(e->h_data.ensure(std::max<uint64_t>(len, 64) + 64));
-    HIP_TRY(e->o_starts.ensure(4));
-    HIP_TRY(e->o_digests.ensure(32));
-    if (len) HIP_TRY(hipMemcpyAsync(e->h_data.p, e->pin_data, len, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(e->o_starts.p, ctl, 16, hipMemcpyHostToDevice, s));
-    HashArgs ha{};
-    ha.zero_page = e->zero_page.p;
-    ha.data = e->h_data.p;
-    ha.uniform_len = 64;  // buffer 0 at offset 0
-    ha.starts = e->o_starts.p;
-    ha.clens = e->o_starts.p + 1;
-    ha.tasks = e->o_starts.p + 2;
-    ha.total = e->o_starts.p + 3;
-    ha.cap = 1;
-    ha.digests = e->o_digests.p;
-    ha.algo = e->prm.hash_algo;
-    HIP_TRY(launch_hash(ha, 1, 0, s));
-    HIP_TRY(hipMemcpyAsync(ctl + 4, e->o_digests.p, 32, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    memcpy(digest, ctl + 4, e->digest_len);
-    return SDFS_CDC_OK;
+    return get_hash_direct(e, data, len, digest);
 }
 
-namespace {
-// fingerprints of n extents on the engine (caller holds e->mu and has set the device)
-int hash_extents(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
-                 const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, hipStream_t s) {
-    if (n_max == 0) return SDFS_CDC_OK;
-    if (n_max > 0xFFFFFFFFull) return fail(SDFS_CDC_EINVAL, "more than 2^32 extents");
-    HIP_TRY(e->x_scratch.ensure(kExtentScratchWords + 2 * n_max));
-    uint32_t* sc = e->x_scratch.p;
-    ExtentArgs xa{d_lens, d_count, n_max, sc + kExtentScratchWords, sc + kExtentScratchWords + n_max,
-                  sc + 1024, sc, sc + 512};
-    HIP_TRY(launch_extent_order(xa, s));
-    HashArgs ha{};
-    ha.zero_page = e->zero_page.p;
-    ha.data = d_data;
-    ha.offs = d_offs;
-    ha.uniform_len = 0;
-    ha.tasks = xa.tasks;
-    ha.total = xa.total;
-    ha.starts = xa.starts;
-    ha.clens = d_lens;
-    ha.cap = 1;
-    ha.digests = d_digests;
-    ha.algo = e->prm.hash_algo;
-    HIP_TRY(launch_hash(ha, n_max, 0, s));
+int sdfs_cdc_queue_stats(sdfs_cdc_engine* e, uint64_t* batches, uint64_t* requests) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    std::lock_guard<std::mutex> lk(e->q_init);
+    if (batches) *batches = e->q ? e->q->batches() : 0;
+    if (requests) *requests = e->q ? e->q->requests() : 0;
     return SDFS_CDC_OK;
 }
-}  // namespace
 
 int sdfs_cdc_host_register(void* p, uint64_t n) {
     if (!p || !n) return fail(SDFS_CDC_EINVAL, "null or empty region");

@@ -22,8 +22,8 @@ struct ScanVariantInfo {
     int lds_bytes;   // LDS image size
     int wg_per_cu;   // resident workgroups per CU the variant is built for
     int blk;         // bytes per lane per iteration (segment length must be a multiple)
-    int fuse;        // resolves cuts in the epilogue when one wave = one buffer (sweep-only:
-                     // measured slower)
+    int fuse;        // cut walk in the epilogue when one wave = one buffer: 1 = from the bitmap
+                     // (sweep only), 2 = from register candidate summaries (production)
 };
 ScanVariantInfo scan_variant_info(int variant);
 
@@ -160,5 +160,12 @@ hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t stream);
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
                         hipStream_t stream);
 bool scan_window_supported(int window);
+
+#ifdef SDFS_TUNING
+// measurement-only variants (cdc_sweep.hip; tuning library only)
+ScanVariantInfo scan_variant_info_sweep(int variant);
+hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t stream);
+hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);
+#endif
 
 }  // namespace sdfs

@@ -11,638 +11,21 @@
 // Reference semantics: VariableSha256HashEngine.getChunks (VariableSha256HashEngine.java:71-86)
 // driving the rabinwindow EnhancedFingerFactory loop; getHash (:58-67).
 // Integer/bit work only: no MFMA (DESIGN.md explains the VALU roofline).
+// This file holds the production configurations only; measured alternatives live in
+// cdc_sweep.hip, which is built into the measurement library (make tuning) and never into
+// libsdfs_cdc.so.
 #include <algorithm>
 
-#include "cdc_internal.h"
+#include "cdc_device.h"
 
 namespace sdfs {
 
-// gfx950 has no v_xor3_b32, but it has v_bitop3_b32 (any 3-input boolean function, truth table
-// 0x96 = a^b^c, 0xE8 = majority); hipcc does not form it for xor chains on its own.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
-}
-// (a & b) | c.  v_bitop3 truth-table bit index is (A << 2) | (B << 1) | C (the encoding hipcc
-// itself emits for Ch, bitop3:0xE4 = C ? A : B).
-__device__ __forceinline__ uint32_t bitop3_and_or(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xEA);
-}
-
-// ------------------------------------------------------------------------------------------
-// 1. candidate scan
-// ------------------------------------------------------------------------------------------
-// One rolling step for byte `inb` (taken from byte p of dword `dw`), popping the byte that left
-// the window (byte q of dword `odw`).  fp = hi:lo (deg < 56).  Equivalent to the jar's
-// pushByte/popByte pair:
-//   j = (fp >> (d-8)) & 0xFF;  fp = ((fp << 8) | b) ^ push[j];  fp ^= pop[o]
-// push[j] carries j*x^d, which cancels the 8 bits shifted above deg-1.
-// Ablation bits (scan sweeps only): 1 = no pop LDS read, 2 = no push LDS read, 4 = no candidate
-// test, 8 = no global loads.  The skipped values are replaced by register values that keep every
-// remaining instruction live.  Bit 16 is not an ablation but a code layout (production): whole
-// blocks are loaded and scanned in a branch of their own (see the scan kernel's block loop).
-template <int P, int Q, int ABL = 0>
-__device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
-                                          uint32_t push_base, uint32_t jshift, const uint8_t* tab) {
-    // push[j] address (j << 8) | push_base with j = (fp >> (d-8)) & 0xFF = hi bits [jshift, jshift+8):
-    // one full-rate shift + one v_bitop3 ((A & B) | C, table 0xEA) instead of v_bfe + v_lshl_or
-    // (both half-rate on gfx950, scripts/isa_microbench.hip).
-    const uint32_t pa = bitop3_and_or(hi >> (jshift - 8), 0xFF00u, push_base);
-    const uint32_t qa = __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + Q) << 8));  // (o << 8) | c8
-    const uint2 pv = (ABL & 2) ? make_uint2(pa, pa >> 3) : *reinterpret_cast<const uint2*>(tab + pa);
-    const uint2 qv = (ABL & 1) ? make_uint2(qa, qa >> 3) : *reinterpret_cast<const uint2*>(tab + qa);
-    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);             // (fp << 8) >> 32
-    const uint32_t nlo = __builtin_amdgcn_perm(lo, dw, 0x06050400u | P);     // (lo << 8) | b
-    lo = xor3(nlo, pv.x, qv.x);
-    hi = xor3(nhi, pv.y, qv.y);
-}
-
-// push-only step (window warm-up from the zero state; no byte leaves the window yet)
-template <int P>
-__device__ __forceinline__ void push_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t push_base,
-                                          uint32_t jshift, const uint8_t* tab) {
-    const uint2 pv = *reinterpret_cast<const uint2*>(tab + bitop3_and_or(hi >> (jshift - 8), 0xFF00u, push_base));
-    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);
-    const uint32_t nlo = __builtin_amdgcn_perm(lo, dw, 0x06050400u | P);
-    lo = nlo ^ pv.x;
-    hi = nhi ^ pv.y;
-}
-
-// Shift the candidate flag of the current position into `bits` (first position ends in the MSB,
-// bit-reversed once per 32 positions).  Written as one v_and/v_cmp/v_addc sequence: in plain C
-// hipcc reassociates the 32 per-byte tests of a word into an OR tree at the end of the word,
-// keeping all 32 fingerprints live (scratch spills on every byte).
-template <bool PRED64>
-__device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t hi, const ScanArgs& a) {
-    uint32_t t;
-    if constexpr (PRED64) {
-        uint32_t t2;
-        asm("v_and_b32 %1, %4, %3\n\t"
-            "v_xor_b32 %1, %5, %1\n\t"
-            "v_and_b32 %2, %7, %6\n\t"
-            "v_xor_b32 %2, %8, %2\n\t"
-            "v_or_b32 %1, %1, %2\n\t"
-            "v_cmp_eq_u32 vcc, 0, %1\n\t"
-            "v_addc_co_u32 %0, vcc, %0, %0, vcc"
-            : "+v"(bits), "=&v"(t), "=&v"(t2)
-            : "v"(lo), "s"(a.mask_lo), "s"(a.val_lo), "v"(hi), "s"(a.mask_hi), "s"(a.val_hi)
-            : "vcc");
-    } else {
-        asm("v_and_b32 %1, %3, %2\n\t"
-            "v_cmp_eq_u32 vcc, %4, %1\n\t"
-            "v_addc_co_u32 %0, vcc, %0, %0, vcc"
-            : "+v"(bits), "=&v"(t)
-            : "v"(lo), "s"(a.mask_lo), "s"(a.val_lo)
-            : "vcc");
-    }
-}
-
-// Byte O of the current block (BLKW dwords), with the byte that leaves the window at O - W: in
-// this block when O >= W, otherwise in `prev` (the previous block's last 64 bytes).
-template <int W, bool PRED64, int O, int ABL, int BLKW>
-__device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& bits, const uint32_t (&cur)[BLKW],
-                                          const uint32_t (&prev)[16], uint32_t c8, uint32_t push_base,
-                                          const uint8_t* tab, const ScanArgs& a) {
-    constexpr int OLD = O - W;  // may be negative -> previous block
-    constexpr int OI = OLD >= 0 ? OLD : OLD + 64;
-    const uint32_t odw = OLD >= 0 ? cur[OI >> 2] : prev[OI >> 2];
-    roll_step<(O & 3), (OI & 3), ABL>(lo, hi, cur[O >> 2], odw, c8, push_base, a.jshift, tab);
-    if constexpr (ABL & 4)
-        bits ^= lo;
-    else
-        cand_shift<PRED64>(bits, lo, hi, a);
-}
-
-#ifndef SDFS_SCAN_SCHED_GROUP
-#define SDFS_SCAN_SCHED_GROUP 4
-#endif
-constexpr int kSchedGroup = SDFS_SCAN_SCHED_GROUP;  // bytes per scheduling region
-
-// Positions O .. O0+31 of one candidate word, all chains interleaved (independent rolling chains
-// give the ILP that hides the LDS latency of the push lookups).
-template <int W, bool PRED64, int O0, int O, int NCH, int ABL, int BLKW>
-__device__ __forceinline__ void word_steps(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
-                                           const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
-                                           uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
-    if constexpr (O < O0 + 32) {
-#pragma unroll
-        for (int c = 0; c < NCH; c++)
-            byte_step<W, PRED64, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
-        // keep the scheduler from hoisting every (chain-independent) pop read of the block
-        // ahead of the rolling chain: that costs ~2 VGPRs per byte and spills.
-        if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) __builtin_amdgcn_sched_barrier(0);
-        word_steps<W, PRED64, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
-    }
-}
-
-template <int W, int O>
-__device__ __forceinline__ void warm_from(uint32_t& lo, uint32_t& hi, const uint32_t (&prev)[16], uint32_t push_base,
-                                          uint32_t jshift, const uint8_t* tab) {
-    if constexpr (O < 64) {
-        push_step<(O & 3)>(lo, hi, prev[O >> 2], push_base, jshift, tab);
-        warm_from<W, O + 1>(lo, hi, prev, push_base, jshift, tab);
-    }
-}
-
-// Load N dwords at byte address `addr` if readable up to `lim`; dwords that hold no byte below
-// `lim` read as zero (only a buffer's last block takes the guarded path).
-template <int N>
-__device__ __forceinline__ void load_block(uint32_t (&d)[N], const uint8_t* data, uint64_t addr, uint64_t lim) {
-    const bool full = addr + 4 * N <= lim;
-    if (__all(full)) {
-        const uint4* p = reinterpret_cast<const uint4*>(data + addr);
-#pragma unroll
-        for (int i = 0; i < N / 4; i++) {
-            const uint4 v = p[i];
-            d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
-        }
-    } else {
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(data + addr);
-#pragma unroll
-        for (int i = 0; i < N; i++) d[i] = (addr + 4 * i < lim) ? p[i] : 0u;
-    }
-}
-
-// All candidate words of one block: word WI covers positions 32*WI .. 32*WI+31.
-template <int W, bool PRED64, int WI, int NW, int NCH, int ABL, int BLKW>
-__device__ __forceinline__ void block_words(uint32_t (&words)[NCH][NW], uint32_t (&lo)[NCH], uint32_t (&hi)[NCH],
-                                            const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
-                                            uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
-    if constexpr (WI < NW) {
-        uint32_t bits[NCH];
-#pragma unroll
-        for (int c = 0; c < NCH; c++) bits[c] = 0;
-        word_steps<W, PRED64, 32 * WI, 32 * WI, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
-#pragma unroll
-        for (int c = 0; c < NCH; c++) words[c][WI] = __builtin_bitreverse32(bits[c]);
-        block_words<W, PRED64, WI + 1, NW, NCH, ABL, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
-    }
-}
-
-// Branch-free block load for software prefetch: a block that is not wholly readable (buffer tail,
-// or no block at all) is fetched from the 128-byte device zero page instead, so no control flow
-// separates the load from its use one iteration later (hipcc puts an s_waitcnt vmcnt(0) at
-// every control-flow merge after a load).  `full` records whether the fast load was valid;
-// tail blocks are re-read by fix_block when they become current.
-template <int N>
-__device__ __forceinline__ bool load_block_nb(uint32_t (&d)[N], const uint8_t* data, const uint8_t* zero_page,
-                                              uint64_t addr, uint64_t lim) {
-    const bool full = addr + 4 * N <= lim;
-    const uint4* p = reinterpret_cast<const uint4*>(full ? data + addr : zero_page);
-#pragma unroll
-    for (int i = 0; i < N / 4; i++) {
-        const uint4 v = p[i];
-        d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
-    }
-    return full;
-}
-
-template <int N>
-__device__ __forceinline__ void fix_block(uint32_t (&d)[N], bool full, const uint8_t* data, uint64_t addr,
-                                          uint64_t lim) {
-    if (!__all(full)) {  // rare: some lane's block is a buffer tail
-        if (!full) {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(data + addr);
-#pragma unroll
-            for (int i = 0; i < N; i++) d[i] = (addr + 4 * i < lim) ? p[i] : 0u;
-        }
-    }
-}
-
-// First candidate position in [lo, hi] (buffer-relative), or -1.
-__device__ __forceinline__ int64_t find_first(const uint32_t* bm, uint64_t word0, uint64_t lo, uint64_t hi,
-                                              uint32_t lane) {
-    const uint64_t wlo = lo >> 5, whi = hi >> 5;
-    for (uint64_t wb = wlo; wb <= whi; wb += 64) {
-        const uint64_t w = wb + lane;
-        uint32_t bits = 0;
-        if (w <= whi) {
-            bits = bm[word0 + w];
-            if (w == wlo) bits &= ~0u << (lo & 31);
-            if (w == whi) bits &= (hi & 31) == 31 ? ~0u : ((2u << (hi & 31)) - 1u);
-        }
-        const uint64_t m = __ballot(bits != 0);
-        if (m) {
-            const uint32_t l = __builtin_ctzll(m);
-            const uint32_t b = __shfl(bits, l);
-            return (int64_t)((wb + l) * 32 + __builtin_ctz(b));
-        }
-    }
-    return -1;
-}
-
-// First candidate in [lo, hi] from the global bitmap, each lane testing 8 consecutive words
-// (a wave covers 16 Ki positions per coalesced 2 KiB load).
-__device__ __forceinline__ int64_t find_first_wide(const uint32_t* bm, uint64_t word0, uint32_t lo, uint32_t hi,
-                                                   uint32_t lane) {
-    const uint32_t lo_w = lo >> 5, hi_w = hi >> 5, lo_b = lo & 31, hi_b = hi & 31;
-    for (uint32_t wb = lo_w; wb <= hi_w; wb += 512) {
-        const uint32_t w0 = wb + 8 * lane;
-        uint32_t bits[8];
-        uint32_t any = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t w = w0 + j;
-            uint32_t v = 0;
-            if (w <= hi_w) {
-                v = bm[word0 + w];
-                if (w == lo_w) v &= ~0u << lo_b;
-                if (w == hi_w) v &= hi_b == 31 ? ~0u : ((2u << hi_b) - 1u);
-            }
-            bits[j] = v;
-            any |= v;
-        }
-        const uint64_t m = __ballot(any != 0);
-        if (m) {
-            const uint32_t l = __builtin_ctzll(m);
-            uint32_t jj = 0, bb = 0;
-#pragma unroll
-            for (int j = 7; j >= 0; j--)
-                if (bits[j]) { jj = j; bb = bits[j]; }
-            const uint32_t pos_in = jj * 32 + (bb ? __builtin_ctz(bb) : 0);
-            const uint32_t p = __shfl(pos_in, l);
-            return (int64_t)(wb + 8 * l) * 32 + p;
-        }
-    }
-    return -1;
-}
-
-__device__ __forceinline__ uint32_t sha_blocks(uint32_t len) { return (len + 8) / 64 + 1; }
-
-// Greedy cut walk over one buffer's candidate bits (one wave, wave-uniform control flow):
-// SURVEY.md A.3 — cut at the first candidate with n past min_len, or at max_len, tail last.
-__device__ __forceinline__ void resolve_buffer(const ResolveArgs& a, uint32_t b, uint32_t lane, uint32_t* lhist) {
-    {
-        const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
-        const uint64_t len = a.uniform_len ? a.uniform_len : a.lens[b];
-        const uint64_t word0 = off >> 5;
-        uint64_t start = 0;
-        uint32_t cnt = 0;
-        while (start < len) {
-            const uint64_t lo = start + a.first_off;
-            const uint64_t forced = start + a.max_len - 1;
-            const uint64_t hi = forced < len - 1 ? forced : len - 1;
-            int64_t k = -1;
-            // 64 words per probe: with thousands of short buffers this kernel is throughput-bound and
-            // the 8-word-per-lane search (find_first_wide) measured 2.5x slower here
-            if (lo <= hi) k = find_first(a.bitmap, word0, lo, hi, lane);
-            if (k < 0) k = (int64_t)hi;  // forced cut at max_len, or the tail chunk
-            const uint32_t clen = (uint32_t)(k + 1 - start);
-            if (cnt < a.cap) {
-                if (lane == 0) {
-                    const uint64_t slot = (uint64_t)b * a.cap + cnt;
-                    a.starts[slot] = (uint32_t)start;
-                    a.clens[slot] = clen;
-                    uint32_t bin = sha_blocks(clen) >> a.bin_shift;
-                    bin = bin < a.nbins ? bin : a.nbins - 1;
-                    atomicAdd(&lhist[bin], 1u);
-                }
-            } else if (lane == 0) {
-                atomicOr(a.overflow, 1u);
-            }
-            cnt++;
-            start = (uint64_t)k + 1;
-        }
-        if (lane == 0) a.counts[b] = cnt < a.cap ? cnt : a.cap;
-    }
-}
-
-// Candidate summary of one scan segment: the first kSumCands candidate offsets (segment-relative,
-// u16) shifted into a 128-bit register quadruple, newest in the low half of s[0]; unused slots
-// hold 0xFFFF.  ncand counts every candidate of the segment (> kSumCands = overflow).
-constexpr uint32_t kSumCands = 8;
-
-__device__ __forceinline__ void sum_push(uint32_t (&s)[4], uint32_t& ncand, uint32_t off) {
-    if (ncand < kSumCands) {
-        s[3] = __builtin_amdgcn_alignbit(s[3], s[2], 16);
-        s[2] = __builtin_amdgcn_alignbit(s[2], s[1], 16);
-        s[1] = __builtin_amdgcn_alignbit(s[1], s[0], 16);
-        s[0] = (s[0] << 16) | off;
-    }
-    ncand++;
-}
-
-// Greedy cut walk of buffer b (one wave; lane l scanned segment l of it, seg_len bytes) from
-// the lanes' candidate summaries: the first candidate in [lo, hi] is the smallest candidate of
-// the first lane whose segment holds one there.  A step whose range touches an overflowed
-// segment searches the bitmap instead (same answer; the bitmap is complete).
-__device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint32_t b, uint32_t lane,
-                                                     const uint32_t (&sm)[4], uint32_t ncand, uint32_t ovf_off,
-                                                     uint32_t seg_len, uint32_t* lhist) {
-    const uint32_t len = a.uniform_len;
-    const uint64_t word0 = ((uint64_t)b * len) >> 5;
-    const uint32_t my_base = lane * seg_len;
-    uint32_t cand[kSumCands];
-#pragma unroll
-    for (uint32_t k = 0; k < kSumCands; k++) {
-        const uint32_t v = (sm[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-        cand[k] = v == 0xFFFFu ? 0xFFFFFFFFu : my_base + v;
-    }
-    const bool ovf = ncand > kSumCands;
-    uint32_t start = 0, cnt = 0;
-    while (start < len) {
-        const uint32_t lo = start + a.first_off;
-        const uint32_t forced = start + a.max_len - 1;
-        const uint32_t hi = forced < len - 1 ? forced : len - 1;
-        int64_t k = -1;
-        if (lo <= hi) {
-            uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-            for (uint32_t j = 0; j < kSumCands; j++) {
-                const uint32_t c = cand[j];
-                if (c >= lo && c <= hi && c < best) best = c;
-            }
-            // an overflowed segment's later candidates (after its 8th) are in the bitmap words
-            // the scan stored from block ovf_off on; a summary hit precedes all of them
-            if (ovf && best == 0xFFFFFFFFu) {
-                uint32_t x = my_base + ovf_off > lo ? my_base + ovf_off : lo;
-                const uint32_t seg_hi = my_base + seg_len - 1;
-                const uint32_t to = seg_hi < hi ? seg_hi : hi;
-                while (x <= to) {
-                    uint32_t w = a.bitmap[word0 + (x >> 5)] >> (x & 31);
-                    const uint32_t span = to - x;  // positions x .. to, at most 32 of them in this word
-                    if (span < 31) w &= (2u << span) - 1u;
-                    if (w) { best = x + __builtin_ctz(w); break; }
-                    x = (x | 31u) + 1u;
-                }
-            }
-            const uint64_t m = __ballot(best != 0xFFFFFFFFu);
-            if (m) k = (int64_t)__builtin_amdgcn_readlane(best, (int)__builtin_ctzll(m));
-        }
-        if (k < 0) k = (int64_t)hi;  // forced cut at max_len, or the tail chunk
-        const uint32_t clen = (uint32_t)(k + 1 - start);
-        if (cnt < a.cap) {
-            if (lane == 0) {
-                const uint64_t slot = (uint64_t)b * a.cap + cnt;
-                a.starts[slot] = start;
-                a.clens[slot] = clen;
-                uint32_t bin = sha_blocks(clen) >> a.bin_shift;
-                bin = bin < a.nbins ? bin : a.nbins - 1;
-                atomicAdd(&lhist[bin], 1u);
-            }
-        } else if (lane == 0) {
-            atomicOr(a.overflow, 1u);
-        }
-        cnt++;
-        start = (uint32_t)k + 1;
-    }
-    if (lane == 0) a.counts[b] = cnt < a.cap ? cnt : a.cap;
-}
-
-// Scan variants (DESIGN.md "Rabin scan"): C lane-private table copies (32: conflict-free,
-// 128 KiB, one 1024-thread workgroup per CU; 16: 2-way, 64 KiB, two workgroups per CU), NCH
-// independent segments per lane, BLK bytes per lane per iteration (128 = one whole cache line
-// per lane per load, so no line is fetched twice), PF = prefetch the next block.
-// FUSE: 0 = separate resolve kernel; 1 = each wave walks its buffer's bitmap in the epilogue
-// (sweep only, measured slower); 2 = each lane keeps its segment's first kSumCands candidate
-// offsets in registers while it scans, and the wave resolves its buffer from them in the epilogue
-// (no bitmap reads unless a segment overflows: DESIGN.md §4).
-template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64, int FUSE = 0>
-struct ScanCfg {
-    static constexpr int kFuse = NCH == 1 ? FUSE : 0;  // resolve each wave's buffer in the epilogue
-    static constexpr int kAbl = ABL;
-    static constexpr int kCopies = C;
-    static constexpr int kChains = NCH;
-    static constexpr bool kPrefetch = PF;
-    static constexpr int kWavesPerSimd = WPS;  // __launch_bounds__ occupancy request
-    static constexpr int kLds = scan_lds_bytes(C);
-    static constexpr uint32_t kPushOff = C == 32 ? 0x10000u : 0x80u;
-    static constexpr int kBlk = BLK;
-};
-
-template <int W, bool PRED64, class CFG>
-__global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
-    constexpr int NCH = CFG::kChains;
-    constexpr int C = CFG::kCopies;
-    constexpr int BLK = CFG::kBlk;
-    constexpr int BLKW = BLK / 4;
-    __shared__ __attribute__((aligned(16))) uint8_t tab[CFG::kLds];
-    __shared__ uint32_t lhist[CFG::kFuse ? kMaxBins : 1];  // fused resolve: chunk-length histogram
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(a.tab_image);
-        uint4* dst = reinterpret_cast<uint4*>(tab);
-        for (int i = threadIdx.x; i < CFG::kLds / 16; i += kScanThreads) dst[i] = src[i];
-        if constexpr (CFG::kFuse != 0)
-            for (uint32_t i = threadIdx.x; i < kMaxBins; i += kScanThreads) lhist[i] = 0;
-    }
-    __syncthreads();
-
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c8 = (lane & (C - 1)) << 3;
-    const uint32_t push_base = CFG::kPushOff | c8;
-    const uint64_t total = a.uniform_len ? a.total_segs : a.seg_prefix[a.nbuf];
-    const uint64_t per_iter = (uint64_t)kScanThreads * NCH;
-
-    for (uint64_t base = (uint64_t)blockIdx.x * per_iter; base < total; base += (uint64_t)gridDim.x * per_iter) {
-        uint64_t start[NCH], end[NCH];
-        uint32_t nblk[NCH];
-        bool first[NCH];
-        uint32_t maxblk = 0;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            const uint64_t seg = base + (uint64_t)c * kScanThreads + threadIdx.x;
-            start[c] = end[c] = 0;
-            nblk[c] = 0;
-            first[c] = true;
-            if (seg < total) {
-                uint64_t bstart, blen, sidx;
-                if (a.uniform_len) {
-                    const uint64_t spb = (a.uniform_len + a.seg_len - 1) / a.seg_len;
-                    const uint64_t b = seg / spb;
-                    sidx = seg - b * spb;
-                    bstart = b * a.uniform_len;
-                    blen = a.uniform_len;
-                } else {
-                    uint32_t lo_b = 0, hi_b = a.nbuf;  // last b with seg_prefix[b] <= seg
-                    while (hi_b - lo_b > 1) {
-                        const uint32_t mid = (lo_b + hi_b) >> 1;
-                        if (a.seg_prefix[mid] <= seg) lo_b = mid; else hi_b = mid;
-                    }
-                    sidx = seg - a.seg_prefix[lo_b];
-                    bstart = a.offs[lo_b];
-                    blen = a.lens[lo_b];
-                }
-                start[c] = bstart + sidx * a.seg_len;
-                const uint64_t bend = bstart + blen;
-                end[c] = start[c] + a.seg_len < bend ? start[c] + a.seg_len : bend;
-                nblk[c] = (uint32_t)((end[c] - start[c] + BLK - 1) / BLK);
-                // window warm-up reads the previous 64 bytes unless this is the buffer's first segment
-                first[c] = start[c] == bstart;
-            }
-            maxblk = nblk[c] > maxblk ? nblk[c] : maxblk;
-        }
-
-        uint32_t lo[NCH], hi[NCH];
-        uint32_t prev[NCH][16], cur[NCH][BLKW];
-        bool cur_full[NCH];
-        uint32_t sm[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};  // FUSE == 2: candidate summary
-        uint32_t ncand = 0;
-        uint32_t ovf_off = 0xFFFFFFFFu;  // FUSE == 2: segment offset of the first stored bitmap block
-        // FUSE == 2 with the fused resolve: bitmap words are stored only once a lane's summary has
-        // overflowed (> kSumCands candidates), from that block on; resolve_from_summary reads them
-        // only there.  Saves the 0.5 GB of bitmap writes per 4 GiB.
-        const bool sparse_bm = CFG::kFuse == 2 && a.fuse_resolve;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            if (nblk[c] != 0 && !first[c]) {
-                load_block<16>(prev[c], a.data, start[c] - 64, start[c]);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 16; i++) prev[c][i] = 0;  // bytes before the buffer are empty
-            }
-            lo[c] = hi[c] = 0;
-            warm_from<W, 64 - W>(lo[c], hi[c], prev[c], push_base, a.jshift, tab);
-            if constexpr (CFG::kPrefetch) {
-                const bool act = nblk[c] != 0;
-                cur_full[c] = load_block_nb<BLKW>(cur[c], a.data, a.zero_page, act ? start[c] : 0, act ? end[c] : 0);
-            }
-        }
-
-        for (uint32_t blk = 0; blk < maxblk; blk++) {
-            uint32_t nxt[NCH][CFG::kPrefetch ? BLKW : 1];
-            bool nxt_full[NCH];
-            uint32_t words[NCH][BLK / 32];
-            bool split_fast = false;
-            if constexpr (CFG::kAbl & 16) {
-                // split body: when every lane's block is whole, a branch of its own loads and
-                // scans it, so no control-flow merge sits between the loads and their uses (hipcc
-                // waits for all 16 loads at such a merge; here it waits per 64 bytes scanned).
-                // Interleaved A/B: 1.59 -> 1.52 ms per 4 GiB (profiles/r01/probes/scan_split_body_ab.jsonl)
-                bool full = true;
-#pragma unroll
-                for (int c = 0; c < NCH; c++)
-                    full = full && blk < nblk[c] && start[c] + (uint64_t)BLK * (blk + 1) <= end[c];
-                split_fast = __all(full);
-                if (split_fast) {
-#pragma unroll
-                    for (int c = 0; c < NCH; c++) {
-                        const uint4* p = reinterpret_cast<const uint4*>(a.data + start[c] + (uint64_t)BLK * blk);
-#pragma unroll
-                        for (int i = 0; i < BLKW / 4; i++) {
-                            const uint4 v = p[i];
-                            cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
-                        }
-                    }
-                    block_words<W, PRED64, 0, BLK / 32, NCH, 0, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
-                }
-            }
-            if (!split_fast) {
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                if constexpr (CFG::kPrefetch) {
-                    fix_block<BLKW>(cur[c], cur_full[c], a.data, start[c] + (uint64_t)BLK * blk, end[c]);
-                    const bool act = blk + 1 < nblk[c];
-                    nxt_full[c] = load_block_nb<BLKW>(nxt[c], a.data, a.zero_page,
-                                                      act ? start[c] + (uint64_t)BLK * (blk + 1) : 0, act ? end[c] : 0);
-                } else if constexpr (CFG::kAbl & 8) {
-#pragma unroll
-                    for (int i = 0; i < BLKW; i++) cur[c][i] = prev[c][i & 15] * 0x9E3779B1u + blk;
-                } else {
-                    const bool act = blk < nblk[c];
-                    load_block<BLKW>(cur[c], a.data, act ? start[c] + (uint64_t)BLK * blk : 0, act ? end[c] : 0);
-                }
-            }
-            block_words<W, PRED64, 0, BLK / 32, NCH, CFG::kAbl & 15, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
-            }
-            if constexpr (CFG::kFuse == 2) {
-                // candidates are rare (~1 per 4 KiB): a divergent, seldom-taken append
-#pragma unroll
-                for (int w = 0; w < BLK / 32; w++) {
-                    uint32_t bits = blk < nblk[0] ? words[0][w] : 0u;
-                    while (bits) {
-                        const uint32_t off = blk * BLK + 32 * w + __builtin_ctz(bits);
-                        bits &= bits - 1;
-                        if (start[0] + off < end[0]) sum_push(sm, ncand, off);
-                    }
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                if constexpr (CFG::kFuse == 2)
-                    if (ncand > kSumCands && ovf_off == 0xFFFFFFFFu) ovf_off = blk * BLK;
-                if (blk < nblk[c] && (!sparse_bm || ncand > kSumCands)) {
-                    const uint64_t pos = start[c] + (uint64_t)BLK * blk;
-                    uint32_t* bm = a.bitmap + (pos >> 5);
-                    if (pos + BLK <= end[c]) {
-                        if constexpr (BLK >= 128) {
-#pragma unroll
-                            for (int w = 0; w < BLK / 32; w += 4)
-                                *reinterpret_cast<uint4*>(bm + w) =
-                                    make_uint4(words[c][w], words[c][w + 1], words[c][w + 2], words[c][w + 3]);
-                        } else {
-                            *reinterpret_cast<uint2*>(bm) = make_uint2(words[c][0], words[c][1]);
-                        }
-                    } else {
-                        // buffer tail: words past the buffer end may belong to the next buffer
-#pragma unroll
-                        for (int w = 0; w < BLK / 32; w++)
-                            if (pos + 32 * w < end[c]) bm[w] = words[c][w];
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < 16; i++) prev[c][i] = cur[c][BLKW - 16 + i];
-                if constexpr (CFG::kPrefetch) {
-#pragma unroll
-                    for (int i = 0; i < BLKW; i++) cur[c][i] = nxt[c][i];
-                    cur_full[c] = nxt_full[c];
-                }
-            }
-        }
-        if constexpr (CFG::kFuse != 0) {
-            if (a.fuse_resolve) {
-                // this wave's 64 segments are buffer seg0 / 64: make the lanes' bitmap stores
-                // visible to the whole wave (same CU, so no L1 staleness), then walk its cuts
-                const uint64_t seg0 = base + (threadIdx.x & ~63u);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                if constexpr (CFG::kFuse == 2) {
-                    if (seg0 < total)
-                        resolve_from_summary(a.res, (uint32_t)(seg0 >> 6), lane, sm, ncand, ovf_off, a.seg_len, lhist);
-                } else {
-                    if (seg0 < total) resolve_buffer(a.res, (uint32_t)(seg0 >> 6), lane, lhist);
-                }
-            }
-        }
-    }
-    if constexpr (CFG::kFuse != 0) {
-        if (a.fuse_resolve) {
-            __syncthreads();
-            for (uint32_t i = threadIdx.x; i < a.res.nbins; i += kScanThreads)
-                if (lhist[i]) atomicAdd(&a.res.hist[i], lhist[i]);
-        }
-    }
-}
-
-// variant table (id 0 = production default; the others are built only for sweeps).  Production:
-// 32 conflict-free table copies, one segment per lane, two whole 128-byte lines per lane per
-// iteration (interleaved A/B on MI355X, scripts/ab.py: 1.56 ms / 4 GiB vs 1.78 ms with one line
-// (variant 7) and 2.6 ms with 64-byte loads; DESIGN.md "Scan variants").
-using ScanV0 = ScanCfg<32, 1, false, 4, 16, 256, 2>;  // + split fast-path body (ABL bit 16, below)
-using ScanV21 = ScanCfg<32, 1, false, 4, 0, 256, 2>;  // + cut resolution from register summaries
-using ScanV20 = ScanCfg<32, 1, false, 4, 0, 256>;    // production before the fused resolve
-using ScanV16 = ScanCfg<32, 2, false, 4>;  // round-1 first version: 64-byte loads, 2 chains
-using ScanV17 = ScanCfg<32, 2, true, 4, 0, 128>;
-using ScanV1 = ScanCfg<32, 2, true, 4>;
-using ScanV2 = ScanCfg<32, 1, true, 4>;
-using ScanV3 = ScanCfg<16, 1, true, 8>;
-using ScanV4 = ScanCfg<16, 1, false, 8>;
-using ScanV5 = ScanCfg<16, 2, false, 4>;
-using ScanV6 = ScanCfg<32, 2, false, 4, 0, 128>;
-using ScanV7 = ScanCfg<32, 1, false, 4, 0, 128>;
-using ScanV8 = ScanCfg<16, 1, false, 8, 0, 128>;
-using ScanV9 = ScanCfg<32, 1, true, 4, 0, 128>;
-using ScanV10 = ScanCfg<32, 1, false, 4, 0, 256>;
-using ScanV15 = ScanCfg<32, 2, false, 4, 0, 256>;
-using ScanV19 = ScanCfg<32, 1, false, 4, 0, 128, 1>;  // 128-B blocks + bitmap-walk resolve in the epilogue
-// ablations of the production configuration (ids 11..25)
-using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;   // no pop read
-using ScanA2 = ScanCfg<32, 1, false, 4, 2, 128>;   // no push read
-using ScanA3 = ScanCfg<32, 1, false, 4, 3, 128>;   // no LDS at all
-using ScanA4 = ScanCfg<32, 1, false, 4, 4, 128>;   // no candidate test
-using ScanA8 = ScanCfg<32, 1, false, 4, 8, 128>;   // no global loads
-using ScanA15 = ScanCfg<32, 1, false, 4, 15, 128>; // only the rolling arithmetic
+// Production scan configuration: 32 conflict-free lane-private table copies (128 KiB of LDS,
+// one 1024-thread workgroup per CU), one 4 KiB segment per lane, 256-byte blocks (two whole
+// 128-byte lines per lane per iteration, so no line is fetched twice), the split fast-path
+// body (ABL bit 16) and the cut walk fused into the epilogue from register summaries (FUSE 2).
+// Interleaved A/B on MI355X against the alternatives is in DESIGN.md §7-8.
+using ScanProd = ScanCfg<32, 1, false, 4, 16, 256, 2>;
 
 template <class CFG>
 constexpr ScanVariantInfo info_of() {
@@ -650,34 +33,12 @@ constexpr ScanVariantInfo info_of() {
 }
 
 ScanVariantInfo scan_variant_info(int v) {
-    switch (v) {
-    case 0: return info_of<ScanV0>();
-#ifdef SDFS_SCAN_SWEEP
-    case 1: return info_of<ScanV1>();
-    case 2: return info_of<ScanV2>();
-    case 3: return info_of<ScanV3>();
-    case 4: return info_of<ScanV4>();
-    case 5: return info_of<ScanV5>();
-    case 6: return info_of<ScanV6>();
-    case 7: return info_of<ScanV7>();
-    case 8: return info_of<ScanV8>();
-    case 9: return info_of<ScanV9>();
-    case 10: return info_of<ScanV10>();
-    case 15: return info_of<ScanV15>();
-    case 16: return info_of<ScanV16>();
-    case 17: return info_of<ScanV17>();
-    case 19: return info_of<ScanV19>();
-    case 20: return info_of<ScanV20>();
-    case 21: return info_of<ScanV21>();
-    case 11: return info_of<ScanA1>();
-    case 12: return info_of<ScanA2>();
-    case 13: return info_of<ScanA3>();
-    case 14: return info_of<ScanA4>();
-    case 18: return info_of<ScanA8>();
-    case 25: return info_of<ScanA15>();
+    if (v == 0) return info_of<ScanProd>();
+#ifdef SDFS_TUNING
+    return scan_variant_info_sweep(v);
+#else
+    return {0, 0, 0, 0, 0, 0};
 #endif
-    default: return {0, 0, 0, 0, 0, 0};
-    }
 }
 
 bool scan_window_supported(int window) {
@@ -693,30 +54,19 @@ static hipError_t launch_scan_wc(const ScanArgs& a, bool pred64, int grid, hipSt
     return hipGetLastError();
 }
 
-template <class CFG>
-static hipError_t launch_scan_c(const ScanArgs& a, int window, bool pred64, int grid, hipStream_t s) {
-    switch (window) {
-    case 16: return launch_scan_wc<16, CFG>(a, pred64, grid, s);
-    case 32: return launch_scan_wc<32, CFG>(a, pred64, grid, s);
-    case 48: return launch_scan_wc<48, CFG>(a, pred64, grid, s);
-    case 64: return launch_scan_wc<64, CFG>(a, pred64, grid, s);
-    default: return hipErrorInvalidValue;
-    }
-}
-
 hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t s) {
-    switch (variant) {
-    case 0: return launch_scan_c<ScanV0>(a, window, pred64, grid, s);
-
-#ifdef SDFS_SCAN_SWEEP
-#define SWEEP_CASE(id, T) \
-    case id: return window == 48 ? launch_scan_wc<48, T>(a, pred64, grid, s) : hipErrorInvalidValue;
-    SWEEP_CASE(1, ScanV1) SWEEP_CASE(2, ScanV2) SWEEP_CASE(3, ScanV3) SWEEP_CASE(4, ScanV4)
-    SWEEP_CASE(5, ScanV5) SWEEP_CASE(6, ScanV6) SWEEP_CASE(7, ScanV7) SWEEP_CASE(8, ScanV8)
-    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16) SWEEP_CASE(17, ScanV17) SWEEP_CASE(19, ScanV19) SWEEP_CASE(20, ScanV20) SWEEP_CASE(21, ScanV21) SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3)
-    SWEEP_CASE(14, ScanA4) SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15)
-#undef SWEEP_CASE
+    if (variant != 0) {
+#ifdef SDFS_TUNING
+        return launch_scan_sweep(a, window, pred64, variant, grid, s);
+#else
+        return hipErrorInvalidValue;
 #endif
+    }
+    switch (window) {
+    case 16: return launch_scan_wc<16, ScanProd>(a, pred64, grid, s);
+    case 32: return launch_scan_wc<32, ScanProd>(a, pred64, grid, s);
+    case 48: return launch_scan_wc<48, ScanProd>(a, pred64, grid, s);
+    case 64: return launch_scan_wc<64, ScanProd>(a, pred64, grid, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1175,320 +525,19 @@ hipError_t launch_scatter(const ScatterArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------------------------------------
-// 5. per-chunk fingerprint: one lane per chunk (tasks are sorted longest-first so the lanes of
-//    a wave carry near-equal block counts)
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
-
-constexpr uint32_t kSha256K[64] = {
-    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
-    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
-    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
-    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
-    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
-    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
-    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
-    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-
-// SHA-256 compression (FIPS 180-4 6.2.2) on 16 big-endian message words; rotations map to
-// v_alignbit_b32, the Sigma xors and Ch/Maj to v_bitop3_b32, the three-input sums to v_add3_u32.
-// SB (sweep builds): a scheduling barrier after every round, so hipcc cannot overlap rounds
-// (lower register pressure, less ILP).
-template <bool SB = false>
-__device__ __forceinline__ void sha256_compress(uint32_t (&s)[8], uint32_t (&w)[16]) {
-    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
-#pragma clang loop unroll(full)
-    for (int i = 0; i < 64; i++) {
-        if (i >= 16 && (i & 15) == 0) {
-            // Message schedule for rounds i..i+15, in place over the 16-word window.  The empty
-            // asm ties the window to the round state so hipcc cannot hoist all of W[16..63]
-            // above the rounds (48 live VGPRs, occupancy 3); it emits no instruction and, since
-            // the old window is dead afterwards, no copies.
-            asm("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
-                "+v"(w[7]), "+v"(w[8]), "+v"(w[9]), "+v"(w[10]), "+v"(w[11]), "+v"(w[12]), "+v"(w[13]),
-                "+v"(w[14]), "+v"(w[15]) : "v"(a));
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-                w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
-            }
-        }
-        const uint32_t wi = w[i & 15];
-        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-        const uint32_t ch = (e & f) | (~e & g);
-        const uint32_t t1 = h + S1 + ch + kSha256K[i] + wi;
-        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-        const uint32_t mj = maj3(a, b, c);
-        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
-        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
-    }
-    s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
-}
-
-__device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
-
-// MD5 compression (RFC 1321 3.4) on 16 little-endian words.
-__device__ __forceinline__ void md5_compress(uint32_t (&s)[4], const uint32_t (&m)[16]) {
-    constexpr uint32_t K[64] = {
-        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
-        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
-        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
-        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
-        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
-        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
-        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
-        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
-    constexpr int R[16] = {7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21};
-    uint32_t a = s[0], b = s[1], c = s[2], d = s[3];
-#pragma unroll
-    for (int i = 0; i < 64; i++) {
-        uint32_t f;
-        int g;
-        if (i < 16) { f = (b & c) | (~b & d); g = i; }
-        else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) & 15; }
-        else if (i < 48) { f = xor3(b, c, d); g = (3 * i + 5) & 15; }
-        else { f = c ^ (b | ~d); g = (7 * i) & 15; }
-        const uint32_t t = a + f + K[i] + m[g];
-        a = d; d = c; c = b;
-        b = b + rotl(t, R[(i >> 4) * 4 + (i & 3)]);
-    }
-    s[0] += a; s[1] += b; s[2] += c; s[3] += d;
-}
-
-// The chunk's final 1-2 blocks: bytes [0, rem) from `t`, the 0x80 terminator, zero fill and the
-// 64-bit bit length (big-endian for SHA-256, little-endian for MD5).  Only aligned dwords that
-// hold at least one chunk byte are read.
-template <bool SHA>
-__device__ __forceinline__ void tail_words(uint32_t (&m)[16], const uint8_t* t, uint32_t rem) {
-    const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(t) & 3);
-    // pointer arithmetic (not an integer round trip) keeps the global address space: global_load,
-    // not flat_load
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(t - r);
-    const uint32_t nd = (r + rem + 3) >> 2;
-    uint32_t d[17];
-#pragma unroll
-    for (int j = 0; j < 17; j++) d[j] = (uint32_t)j < nd ? q[j] : 0u;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        uint32_t v = __builtin_amdgcn_alignbyte(d[j + 1], d[j], r);  // little-endian bytes t[4j..4j+3]
-        const int k = (int)rem - 4 * j;
-        if (k <= 0) v = 0;
-        else if (k < 4) v &= (1u << (8 * k)) - 1u;
-        if (k >= 0 && k < 4) v |= 0x80u << (8 * k);
-        m[j] = SHA ? __builtin_bswap32(v) : v;
-    }
-}
-
-__device__ __forceinline__ void load_block64(uint4 (&v)[4], const uint8_t* q) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) __builtin_memcpy(&v[j], q + 16 * j, 16);  // unaligned global_load_dwordx4
-}
-
-// ABL (sweep builds only): 1 = synthesize the message words instead of loading them, 2 = skip the
-// compression (fold the loaded words instead), 4 = read from the chunk start rounded down to 128 B
-// (wrong digests; every line is fetched once: the cost of the unaligned-line re-fetch).
-// Production ABL = 0.
-// BS = threads per workgroup; PF = load data block blk+1 while block blk is compressed.
-template <int ALGO, int ABL, bool PF>
-__device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
-    constexpr bool SHA = ALGO != 2;
-    const uint32_t slot = a.tasks[i];
-    const uint32_t b = slot / a.cap;
-    const uint32_t k = slot - b * a.cap;
-    const uint64_t boff = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
-    const uint32_t cs = a.starts[slot];
-    const uint32_t len = a.clens[slot];
-    const uint8_t* p = a.data + boff + cs;
-    if constexpr ((ABL & 4) != 0) p = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(127));
-    const uint32_t nfull = len >> 6;           // whole 64-byte data blocks
-    const uint32_t nblocks = (len + 8) / 64 + 1;  // + terminator/length block(s)
-    const uint64_t bits = (uint64_t)len * 8;
-    uint32_t s[8];
-    if constexpr (SHA) {
-        s[0] = 0x6a09e667; s[1] = 0xbb67ae85; s[2] = 0x3c6ef372; s[3] = 0xa54ff53a;
-        s[4] = 0x510e527f; s[5] = 0x9b05688c; s[6] = 0x1f83d9ab; s[7] = 0x5be0cd19;
-    } else {
-        s[0] = 0x67452301; s[1] = 0xefcdab89; s[2] = 0x98badcfe; s[3] = 0x10325476;
-        s[4] = s[5] = s[6] = s[7] = 0;
-    }
-    // One compression per block; lanes of a wave hold chunks of near-equal block count
-    // (longest-first binning), so the data/tail branch below is wave-uniform almost always.
-    // ABL bit 16 (with PF): the next block's load is unconditional (the zero page past the last
-    // whole block), so the loop-carried registers need no copy at the data/tail merge; with the
-    // load inside the branch, hipcc copied the new block into place before the compression and
-    // so waited for it there (s_waitcnt vmcnt right after issuing: no prefetch at all).
-    constexpr bool kPF2 = PF && (ABL & 16);
-    uint4 nx[4];
-    if constexpr (kPF2) {
-        load_block64(nx, nfull ? p : a.zero_page);
-    } else if constexpr (PF) {
-        if (nfull) load_block64(nx, p);  // block 0 (a chunk shorter than 64 B has none to read)
-    }
-    for (uint32_t blk = 0; blk < nblocks; blk++) {
-        uint32_t w[16];
-        uint4 pf_cur[4];
-        if constexpr (kPF2) {
-#pragma unroll
-            for (int q = 0; q < 4; q++) pf_cur[q] = nx[q];
-            load_block64(nx, blk + 1 < nfull ? p + 64 * (blk + 1) : a.zero_page);
-        }
-        if (blk < nfull) {
-            uint4 cur[4];
-            if constexpr (kPF2) {
-#pragma unroll
-                for (int q = 0; q < 4; q++) cur[q] = pf_cur[q];
-            } else if constexpr (PF) {
-#pragma unroll
-                for (int q = 0; q < 4; q++) cur[q] = nx[q];
-                // next block, clamped to the last full one so the load stays branch-free and in bounds
-                const uint32_t nb = blk + 1 < nfull ? blk + 1 : blk;
-                load_block64(nx, p + 64 * nb);
-            } else if constexpr (!(ABL & 1)) {
-                load_block64(cur, p + 64 * blk);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                uint4 v;
-                if constexpr (ABL & 1)
-                    v = make_uint4(s[q] + blk, s[q + 4] ^ blk, s[q] * 3u, s[q + 4] + q);
-                else
-                    v = cur[q];
-                w[4 * q] = SHA ? __builtin_bswap32(v.x) : v.x;
-                w[4 * q + 1] = SHA ? __builtin_bswap32(v.y) : v.y;
-                w[4 * q + 2] = SHA ? __builtin_bswap32(v.z) : v.z;
-                w[4 * q + 3] = SHA ? __builtin_bswap32(v.w) : v.w;
-            }
-        } else {
-            if (blk == nfull) {
-                tail_words<SHA>(w, p + 64 * nfull, len & 63);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 16; j++) w[j] = 0;
-            }
-            if (blk == nblocks - 1) {
-                w[14] = SHA ? (uint32_t)(bits >> 32) : (uint32_t)bits;
-                w[15] = SHA ? (uint32_t)bits : (uint32_t)(bits >> 32);
-            }
-        }
-        if constexpr (ABL & 2) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) s[j & 7] ^= w[j];
-        } else if constexpr (SHA) {
-            sha256_compress<(ABL & 8) != 0>(s, w);
-        } else {
-            uint32_t m4[4] = {s[0], s[1], s[2], s[3]};
-            md5_compress(m4, w);
-            s[0] = m4[0]; s[1] = m4[1]; s[2] = m4[2]; s[3] = m4[3];
-        }
-    }
-    uint32_t dig[8];
-    if constexpr (SHA) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) dig[j] = __builtin_bswap32(s[j]);
-        if constexpr (ALGO == 1) dig[5] = dig[6] = dig[7] = 0;  // VARIABLE_SHA256_160: first 20 bytes
-    } else {
-        dig[0] = s[0]; dig[1] = s[1]; dig[2] = s[2]; dig[3] = s[3];
-        dig[4] = dig[5] = dig[6] = dig[7] = 0;
-    }
-    uint4* out = reinterpret_cast<uint4*>(a.digests + (uint64_t)slot * 32);
-    const uint4 d0 = make_uint4(dig[0], dig[1], dig[2], dig[3]);
-    const uint4 d1 = make_uint4(dig[4], dig[5], dig[6], dig[7]);
-    out[0] = d0;
-    out[1] = d1;
-    if (a.records) {
-        const uint64_t r = (uint64_t)a.rec_base[b] + k;
-        if (r < a.records_cap) {
-            uint4* rec = reinterpret_cast<uint4*>(a.records + r * kRecordBytes);
-            const uint64_t id = a.buffer_id_base + b;
-            rec[0] = d0;
-            rec[1] = d1;
-            rec[2] = make_uint4((uint32_t)id, (uint32_t)(id >> 32), cs, len);
-        }
-    }
-}
-
-// PRIO: a wave whose chunks are long raises its issue priority.  A chunk's SHA-256 is a serial
-// chain of ~1.4 k VALU instructions per 64-byte block (~2 us per block at full issue rate), so
-// the longest chunk of a batch (up to 2049 blocks with the backup profile's 128 KiB maxLen)
-// sets a floor under the kernel unless its wave is not slowed by the waves sharing its SIMD.
-// WPE: minimum waves per SIMD the register allocation must allow (0 = compiler's choice).
-template <int ALGO, int ABL = 0, int BS = 256, bool PF = false, bool PRIO = false, int WPE = 0>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1, 8)))
-void chunk_hash_kernel(HashArgs a) {
-    const uint32_t i = blockIdx.x * BS + threadIdx.x;
-    if (i >= *a.total) return;
-    if constexpr (PRIO) {
-        const uint32_t nb = __builtin_amdgcn_readfirstlane(sha_blocks(a.clens[a.tasks[i]]));
-        if (nb > 1024)
-            __builtin_amdgcn_s_setprio(3);
-        else if (nb > 512)
-            __builtin_amdgcn_s_setprio(2);
-        else if (nb > 256)
-            __builtin_amdgcn_s_setprio(1);
-    }
-    hash_task<ALGO, ABL, PF>(a, i);
-}
-
-// Persistent form: a fixed grid (a.persist_grid workgroups) whose waves take the next 64 tasks
-// of the longest-first list from a counter until it runs dry.  A capped grid leaves register
-// room on every CU for a concurrently running scan (a.wave_ctr is zeroed by the caller).
-template <int ALGO, bool PF>
-__global__ __launch_bounds__(256) void chunk_hash_persistent_kernel(HashArgs a) {
-    const uint32_t total = *a.total;
-    const uint32_t lane = threadIdx.x & 63;
-    for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.wave_ctr, 64u);
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-        if (base >= total) break;
-        if (base + lane < total) hash_task<ALGO, 0, PF>(a, base + lane);
-    }
-}
-
 hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t s) {
     const uint32_t blocks = (uint32_t)((max_tasks + 255) / 256);
     if (blocks == 0) return hipSuccess;
-#ifdef SDFS_SCAN_SWEEP
-    if (a.algo == 0 && variant != 0) {
-        const uint32_t b64 = (uint32_t)((max_tasks + 63) / 64);
-        switch (variant) {
-        case 1: hipLaunchKernelGGL((chunk_hash_kernel<0, 1>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((chunk_hash_kernel<0, 2>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 64, false>), dim3(b64), dim3(64), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 64, true>), dim3(b64), dim3(64), 0, s, a); break;
-        case 6:
-            if (!a.wave_ctr || !a.persist_grid) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((chunk_hash_persistent_kernel<0, true>), dim3(a.persist_grid), dim3(256), 0, s, a);
-            break;
-        case 7:
-            if (!a.wave_ctr || !a.persist_grid) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((chunk_hash_persistent_kernel<0, false>), dim3(a.persist_grid), dim3(256), 0, s, a);
-            break;
-        case 8: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 9: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, false>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 11: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 12: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true, 6>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 13: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 14: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 15: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 16: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 10: hipLaunchKernelGGL((chunk_hash_kernel<0, 4, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
-        // the prefetch before ABL bit 16 (its copy at the data/tail merge waited for the load)
-        case 20: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
-        default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
+    if (variant != 0) {
+#ifdef SDFS_TUNING
+        return launch_hash_sweep(a, max_tasks, variant, s);
+#else
+        return hipErrorInvalidValue;
 #endif
-    if (variant != 0) return hipErrorInvalidValue;
-    // production: next-block prefetch, issued unconditionally (ABL bit 16: interleaved A/B 2.762 ->
-    // 2.744 ms median, 2.725 -> 2.680 min, profiles/r01/probes/hash_true_prefetch_ab.jsonl) (measured ~5 % faster on the B1 length mix, 108 VGPRs) and
-    // issue priority for waves of long chunks (interleaved A/B: 2.75 vs 2.81 ms per 4 GiB,
-    // profiles/r01/probes/hash_prio_ab.jsonl; sweep variant 9 = without)
+    }
+    // production: next-block prefetch issued unconditionally (ABL bit 16; interleaved A/B 2.762 ->
+    // 2.744 ms median, profiles/r01/probes/hash_true_prefetch_ab.jsonl) and issue priority for
+    // waves of long chunks (2.75 vs 2.81 ms per 4 GiB, profiles/r01/probes/hash_prio_ab.jsonl)
     switch (a.algo) {
     case 0: hipLaunchKernelGGL((chunk_hash_kernel<0, 16, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
     case 1: hipLaunchKernelGGL((chunk_hash_kernel<1, 16, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;

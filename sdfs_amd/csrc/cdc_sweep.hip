@@ -1,0 +1,132 @@
+// cdc_sweep.hip — measurement-only kernel variants (scan layouts, ablations, fingerprint-kernel
+// forms) for the A/B sweeps behind DESIGN.md §7-8 (scripts/sweep_scan.py, scripts/ab.py).
+// Built only into the tuning library (`make tuning` -> sdfs_amd/libsdfs_cdc_tuning.so, compiled
+// with -DSDFS_TUNING); the product library libsdfs_cdc.so contains none of these kernels and
+// ignores every SDFS_* tuning variable.
+#include <algorithm>
+
+#include "cdc_device.h"
+
+namespace sdfs {
+
+// scan variants: ScanCfg<copies, chains, prefetch, waves/SIMD, ablation, block bytes, fuse>
+using ScanV21 = ScanCfg<32, 1, false, 4, 0, 256, 2>;  // register-summary resolve without the split body
+using ScanV20 = ScanCfg<32, 1, false, 4, 0, 256>;    // production before the fused resolve
+using ScanV16 = ScanCfg<32, 2, false, 4>;  // round-1 first version: 64-byte loads, 2 chains
+using ScanV17 = ScanCfg<32, 2, true, 4, 0, 128>;
+using ScanV1 = ScanCfg<32, 2, true, 4>;
+using ScanV2 = ScanCfg<32, 1, true, 4>;
+using ScanV3 = ScanCfg<16, 1, true, 8>;
+using ScanV4 = ScanCfg<16, 1, false, 8>;
+using ScanV5 = ScanCfg<16, 2, false, 4>;
+using ScanV6 = ScanCfg<32, 2, false, 4, 0, 128>;
+using ScanV7 = ScanCfg<32, 1, false, 4, 0, 128>;
+using ScanV8 = ScanCfg<16, 1, false, 8, 0, 128>;
+using ScanV9 = ScanCfg<32, 1, true, 4, 0, 128>;
+using ScanV10 = ScanCfg<32, 1, false, 4, 0, 256>;
+using ScanV15 = ScanCfg<32, 2, false, 4, 0, 256>;
+using ScanV19 = ScanCfg<32, 1, false, 4, 0, 128, 1>;  // 128-B blocks + bitmap-walk resolve in the epilogue
+// ablations (ids 11..25): 1 = no pop read, 2 = no push read, 4 = no candidate test, 8 = no
+// global loads; the skipped values are replaced by register values that keep the rest live
+using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;
+using ScanA2 = ScanCfg<32, 1, false, 4, 2, 128>;
+using ScanA3 = ScanCfg<32, 1, false, 4, 3, 128>;
+using ScanA4 = ScanCfg<32, 1, false, 4, 4, 128>;
+using ScanA8 = ScanCfg<32, 1, false, 4, 8, 128>;
+using ScanA15 = ScanCfg<32, 1, false, 4, 15, 128>;
+
+template <class CFG>
+constexpr ScanVariantInfo sweep_info() {
+    return {CFG::kCopies, CFG::kChains, CFG::kLds, CFG::kWavesPerSimd / 4, CFG::kBlk, CFG::kFuse};
+}
+
+ScanVariantInfo scan_variant_info_sweep(int v) {
+    switch (v) {
+    case 1: return sweep_info<ScanV1>();
+    case 2: return sweep_info<ScanV2>();
+    case 3: return sweep_info<ScanV3>();
+    case 4: return sweep_info<ScanV4>();
+    case 5: return sweep_info<ScanV5>();
+    case 6: return sweep_info<ScanV6>();
+    case 7: return sweep_info<ScanV7>();
+    case 8: return sweep_info<ScanV8>();
+    case 9: return sweep_info<ScanV9>();
+    case 10: return sweep_info<ScanV10>();
+    case 15: return sweep_info<ScanV15>();
+    case 16: return sweep_info<ScanV16>();
+    case 17: return sweep_info<ScanV17>();
+    case 19: return sweep_info<ScanV19>();
+    case 20: return sweep_info<ScanV20>();
+    case 21: return sweep_info<ScanV21>();
+    case 11: return sweep_info<ScanA1>();
+    case 12: return sweep_info<ScanA2>();
+    case 13: return sweep_info<ScanA3>();
+    case 14: return sweep_info<ScanA4>();
+    case 18: return sweep_info<ScanA8>();
+    case 25: return sweep_info<ScanA15>();
+    default: return {0, 0, 0, 0, 0, 0};
+    }
+}
+
+template <class T>
+static hipError_t sweep_launch(const ScanArgs& a, bool pred64, int grid, hipStream_t s) {
+    if (pred64)
+        hipLaunchKernelGGL((cdc_scan_kernel<48, true, T>), dim3(grid), dim3(kScanThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((cdc_scan_kernel<48, false, T>), dim3(grid), dim3(kScanThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t s) {
+    if (window != 48) return hipErrorInvalidValue;  // variants are built for the reference window only
+    switch (variant) {
+#define SWEEP_CASE(id, T) \
+    case id: return sweep_launch<T>(a, pred64, grid, s);
+    SWEEP_CASE(1, ScanV1) SWEEP_CASE(2, ScanV2) SWEEP_CASE(3, ScanV3) SWEEP_CASE(4, ScanV4)
+    SWEEP_CASE(5, ScanV5) SWEEP_CASE(6, ScanV6) SWEEP_CASE(7, ScanV7) SWEEP_CASE(8, ScanV8)
+    SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16)
+    SWEEP_CASE(17, ScanV17) SWEEP_CASE(19, ScanV19) SWEEP_CASE(20, ScanV20) SWEEP_CASE(21, ScanV21)
+    SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3) SWEEP_CASE(14, ScanA4)
+    SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15)
+#undef SWEEP_CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// fingerprint-kernel variants (SHA-256 only)
+hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t s) {
+    const uint32_t blocks = (uint32_t)((max_tasks + 255) / 256);
+    if (blocks == 0) return hipSuccess;
+    if (a.algo != 0) return hipErrorInvalidValue;
+    const uint32_t b64 = (uint32_t)((max_tasks + 63) / 64);
+    switch (variant) {
+    case 1: hipLaunchKernelGGL((chunk_hash_kernel<0, 1>), dim3(blocks), dim3(256), 0, s, a); break;    // no loads
+    case 2: hipLaunchKernelGGL((chunk_hash_kernel<0, 2>), dim3(blocks), dim3(256), 0, s, a); break;    // no compression
+    case 3: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 64, false>), dim3(b64), dim3(64), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 64, true>), dim3(b64), dim3(64), 0, s, a); break;
+    case 6:
+        if (!a.wave_ctr || !a.persist_grid) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((chunk_hash_persistent_kernel<0, true>), dim3(a.persist_grid), dim3(256), 0, s, a);
+        break;
+    case 7:
+        if (!a.wave_ctr || !a.persist_grid) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((chunk_hash_persistent_kernel<0, false>), dim3(a.persist_grid), dim3(256), 0, s, a);
+        break;
+    case 8: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 9: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, false>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 11: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 12: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true, 6>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 13: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 14: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, false, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 15: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 16: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 10: hipLaunchKernelGGL((chunk_hash_kernel<0, 4, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    // the prefetch before ABL bit 16 (its copy at the data/tail merge waited for the load)
+    case 20: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace sdfs

@@ -712,6 +712,9 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     z->device = device;
     z->mode = mode;
     z->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+#ifdef SDFS_TUNING
+    // measurement-only layouts (tuning library; DESIGN.md §11 measured them, the product library
+    // reads no environment)
     if (const char* v = getenv("SDFS_LZ4_GTAB")) z->gtab_mode = atoi(v);
     if (z->gtab_mode) z->wg_per_cu = 24;
     if (const char* v = getenv("SDFS_LZ4_STAGE")) z->stage = atoi(v);
@@ -720,6 +723,7 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     if (const char* v = getenv("SDFS_LZ4_DEC_STAGE")) z->dec_stage = atoi(v) == 8192 ? 8192 : (int)kDecStage;
     if (const char* v = getenv("SDFS_LZ4_DEC_WG_PER_CU")) z->dec_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_WG_PER_CU")) z->wg_per_cu = std::max(1, atoi(v));
+#endif
     if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
         delete z;
         return fail_status(SDFS_CDC_EHIP, "stream creation failed");

@@ -76,6 +76,7 @@ class SdfsConfig:
     pred_value: int = 0
     min_cmp: int = MIN_GT
     max_batch_bytes: int = 0  # host-batch pinned staging per slot (0 = the engine default, 256 MiB)
+    direct: bool = False      # SDFS_CDC_FLAG_DIRECT: one GPU round trip per call (no coalescing)
 
     @classmethod
     def backup_volume(cls, **kw) -> "SdfsConfig":
@@ -132,6 +133,7 @@ class SdfsConfig:
         p.pred_value = self.pred_value
         p.min_cmp = self.min_cmp
         p.max_batch_bytes = self.max_batch_bytes
+        p.flags = _lib.FLAG_DIRECT if self.direct else 0
         ht = (hash_type or self.hash_type).upper()
         if ht not in _ALGO:
             raise ValueError(f"hash-type {ht} has no variable engine (HashFunctionPool.java:102-121)")
@@ -277,9 +279,11 @@ class HipVariableSha256HashEngine:
     def sync(self) -> None:
         check(self._lib.sdfs_cdc_stream_sync(self._h))
 
-    def set_pipeline(self, parts: int, part_min_bytes: int = 512 << 20) -> None:
-        """Sub-batch pipelining of run_device (scan of part k+1 overlaps hash of part k)."""
-        check(self._lib.sdfs_cdc_set_pipeline(self._h, int(parts), int(part_min_bytes)))
+    def queue_stats(self) -> tuple[int, int]:
+        """(GPU passes launched, getChunks/getHash calls served) by the coalescing queue."""
+        b, r = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self._lib.sdfs_cdc_queue_stats(self._h, ctypes.byref(b), ctypes.byref(r)))
+        return b.value, r.value
 
     def set_timing(self, nruns: int) -> None:
         """Record HIP events around every kernel of the next runs (ring of `nruns`; 0 = off)."""

@@ -27,6 +27,23 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_tuning_library_exports_the_same_abi():
+    lib = ctypes.CDLL(_lib.TUNING_LIB)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_product_library_reads_no_tuning_environment():
+    """Kernel variants and A/B switches exist only in the tuning library: no SDFS_* variable can
+    change the product's kernels (the product library does not even contain their names)."""
+    prod = open(_lib.DEFAULT_LIB, "rb").read()
+    tuning = open(_lib.TUNING_LIB, "rb").read()
+    for name in (b"SDFS_SCAN_VARIANT", b"SDFS_HASH_VARIANT", b"SDFS_SEG_LEN", b"SDFS_HASH_WG_PER_CU",
+                 b"SDFS_COPY_THREADS", b"SDFS_LZ4_GTAB", b"SDFS_LZ4_STAGE", b"SDFS_AES_VARIANT"):
+        assert name not in prod, name
+        assert name in tuning, name
+
+
 def test_python_binding_covers_header():
     assert set(declared_symbols()) == set(_lib.SIGNATURES)
     _lib.load()  # every signature applied without AttributeError

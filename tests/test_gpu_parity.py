@@ -269,28 +269,72 @@ def test_device_b1_full_size_properties():
     assert 7000 < mean < 9500, mean  # ~8.2 KiB for a 12-bit predicate, min 4095
 
 
-@pytest.mark.parametrize("parts", [1, 3, 7])
-def test_device_subbatch_pipeline_matches(parts):
-    """Sub-batch pipelining (scan of part k+1 on one stream, hash of part k on another) gives the
-    same slots, totals and record table as one part, and matches the oracle."""
+def test_device_two_streams_in_flight_one_engine():
+    """One engine, runs alternating between two streams (two batches in flight: the workspace
+    ring lets one batch's scan overlap the other's fingerprinting).  Every run equals the
+    single-stream result and the oracle."""
     prm = P()
-    e = HipVariableSha256HashEngine(config=SdfsConfig())
-    e.set_pipeline(parts, 1 << 20)
-    batch = DeviceBatch(e, nbuf=300, buf_len=262144)
-    batch.fill_streams(first_stream=200, bufs_per_stream=100)
-    for _ in range(2):  # back-to-back runs on the same stream
-        batch.run(buffer_id_base=7)
-    counts, st, ln, dg, total = batch.host_results()
+    e = HipVariableSha256HashEngine()
+    batches = [DeviceBatch(e, nbuf=300, buf_len=262144) for _ in range(2)]
+    batches[0].fill_streams(first_stream=200, bufs_per_stream=100)
+    batches[1].data = batches[0].data
+    batches[0].run(buffer_id_base=7)
+    ref = batches[0].host_results()
+    ref_rec = batches[0].record_table().cpu().numpy()
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    for _ in range(3):
+        for k in range(6):
+            batches[k % 2].run(buffer_id_base=7, stream=streams[k % 2].cuda_stream)
+    torch.cuda.synchronize()
+    for bt in batches:
+        got = bt.host_results()
+        for x, y in zip(got[:4], ref[:4]):
+            assert np.array_equal(x, y)
+        assert got[4] == ref[4]
+        assert np.array_equal(bt.record_table().cpu().numpy(), ref_rec)
+    counts, st, ln, dg, total = ref
     _check_cover(counts, st, ln, 262144, prm)
-    _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 100, 200, [0, 1, 99, 100, 101, 150, 199, 200, 298, 299])
-    rec = batch.record_table().cpu().numpy()
-    assert rec.shape[0] == total == int(counts.sum())
-    base = np.concatenate([[0], np.cumsum(counts.astype(np.int64))[:-1]]).astype(np.int64)
-    for b in (0, 99, 100, 150, 299):
-        for i in range(counts[b]):
-            r = rec[base[b] + i]
-            assert bytes(r[:32]) == bytes(dg[b, i]) and int.from_bytes(bytes(r[32:40]), "little") == 7 + b
+    _check_batch_against_oracle(batches[0], counts, st, ln, dg, prm, 100, 200, [0, 1, 99, 100, 150, 299])
     e.destroy()
+
+
+def test_device_4k_mean_mix_full_size():
+    """The metric's 4 KiB-mean mix at BASELINE configs[1] size: min-variable-segment-size=2
+    (minLen 2047, Config.java:145-148) and an 11-bit predicate; 4 GiB of 256 KiB buffers.  At
+    ~2 candidates per 4 KiB scan segment a few hundred segments overflow the 8-entry register
+    summary, so the fused walk's bitmap path runs at full size too."""
+    prm = P(min_len=2047, pred_mask=0x7FF)
+    e = engine_for(prm)
+    batch = DeviceBatch(e, nbuf=16384, buf_len=262144)
+    batch.fill_streams(first_stream=0, bufs_per_stream=256)
+    batch.run(buffer_id_base=0)
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    _check_cover(counts, st, ln, 262144, prm)
+    rng = np.random.default_rng(4)
+    sample = sorted(set(rng.integers(0, 16384, 40).tolist()) | {0, 16383})
+    _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 256, 0, sample)
+    mean = 262144 * 16384 / total
+    assert 3800 < mean < 4300, mean  # SURVEY A.4: 4 095 B expected (minus the buffer-end truncation)
+
+
+@pytest.mark.parametrize("mask,min_len", [(0x7FF, 2047), (0x7FF, 1023)])
+def test_device_dense_candidates_11bit(mask, min_len):
+    """Zero runs (every position a candidate) under the 4 KiB-mean parameters: summary overflow
+    mid-segment, across segments, whole buffers and both buffer ends."""
+    prm = P(min_len=min_len, pred_mask=mask)
+    e = engine_for(prm)
+    nbuf, buf_len = 32, 262144
+    host = _dense_candidate_buffers(nbuf, buf_len)
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=buf_len)
+    batch.data.copy_(torch.from_numpy(host.reshape(-1)))
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    for b in range(nbuf):
+        es, el, ed = O.chunk(host[b].tobytes(), O.Params(**prm))
+        c = counts[b]
+        assert st[b, :c].tolist() == es.tolist() and ln[b, :c].tolist() == el.tolist(), b
+        assert (dg[b, :c] == ed).all(), b
 
 
 def test_device_dedup_50pct_copies_are_identical():

@@ -1,0 +1,130 @@
+"""The JNI glue (jni/sdfs_cdc_jni.c, compiled against jni/jni_min.h) driven through a stand-in
+JNIEnv (tests/jni/jni_stub.c): the native methods a JVM would call for
+org.opendedup.hashing.HipVariableSha256HashEngine (jni/HipVariableSha256HashEngine.java), i.e.
+AbstractHashEngine.getChunks / getHash (AbstractHashEngine.java:24-39,
+VariableSha256HashEngine.java:58-86).  CPU tests: symbols and the no-device error path; GPU
+tests: results against the oracle, and the error convention (IOException from getChunks,
+SparseDedupFile.java:578-580)."""
+import ctypes
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cdc_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GLUE = os.path.join(ROOT, "jni", "libsdfs_cdc_jni.so")
+STUB = os.path.join(ROOT, "tests", "jni", "libjni_stub.so")
+PFX = "Java_org_opendedup_hashing_HipVariableSha256HashEngine_"
+NATIVES = ["nativeCreate", "nativeDestroy", "nativeSlotCap", "nativeDigestLen", "nativeGetChunks", "nativeGetHash",
+           "nativeRegister", "nativeLastError"]
+VP = ctypes.c_void_p
+
+
+class Jni:
+    def __init__(self):
+        from sdfs_amd import _lib
+        _lib.load()  # torch's HIP runtime first, then the engine (same order as the package)
+        self.stub = ctypes.CDLL(STUB)
+        self.glue = ctypes.CDLL(GLUE)
+        s = self.stub
+        s.stub_env.restype = VP
+        s.stub_new_array.restype = VP
+        s.stub_new_array.argtypes = [ctypes.c_int, ctypes.c_int32, VP]
+        s.stub_array_data.restype = VP
+        s.stub_array_data.argtypes = [VP]
+        s.stub_free.argtypes = [VP]
+        s.stub_take_exception.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        g = self.glue
+        f = getattr(g, PFX + "nativeCreate")
+        f.restype = ctypes.c_int64
+        f.argtypes = [VP, VP, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                      ctypes.c_int32, ctypes.c_int32]
+        getattr(g, PFX + "nativeDestroy").argtypes = [VP, VP, ctypes.c_int64]
+        for n in ("nativeSlotCap",):
+            getattr(g, PFX + n).argtypes = [VP, VP, ctypes.c_int64, ctypes.c_int32]
+        getattr(g, PFX + "nativeDigestLen").argtypes = [VP, VP, ctypes.c_int64]
+        getattr(g, PFX + "nativeGetChunks").argtypes = [VP, VP, ctypes.c_int64, VP, VP, VP, VP]
+        getattr(g, PFX + "nativeGetHash").argtypes = [VP, VP, ctypes.c_int64, VP, VP]
+        getattr(g, PFX + "nativeRegister").argtypes = [VP, VP, VP]
+        self.env = s.stub_env()
+
+    def call(self, name, *args):
+        return getattr(self.glue, PFX + name)(self.env, None, *args)
+
+    def exception(self):
+        c, m = ctypes.create_string_buffer(128), ctypes.create_string_buffer(512)
+        return (c.value.decode(), m.value.decode()) if self.stub.stub_take_exception(c, 128, m, 512) else None
+
+    def byte_array(self, data: bytes):
+        return self.stub.stub_new_array(1, len(data), data)
+
+    def new(self, kind, n):
+        return self.stub.stub_new_array(kind, n, None)
+
+    def read(self, arr, dtype, n):
+        return np.ctypeslib.as_array(ctypes.cast(self.stub.stub_array_data(arr), ctypes.POINTER(ctypes.c_uint8)),
+                                     (n * np.dtype(dtype).itemsize,)).view(dtype).copy()
+
+
+def test_glue_exports_every_native_method():
+    lib = ctypes.CDLL(GLUE)
+    missing = [n for n in NATIVES if not hasattr(lib, PFX + n)]
+    assert not missing, missing
+    # the Java source declares exactly these natives
+    java = open(os.path.join(ROOT, "jni", "HipVariableSha256HashEngine.java")).read()
+    for n in NATIVES:
+        assert f" {n}(" in java, n
+
+
+def test_create_without_device_throws_ioexception():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    j = Jni()
+    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, 0, 0)
+    assert h == 0
+    cls, msg = j.exception()
+    assert cls == "java/io/IOException" and msg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo", [0, 1, 2])
+def test_jni_get_chunks_and_get_hash_vs_oracle(algo):
+    j = Jni()
+    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, algo, 0)
+    assert h and j.exception() is None
+    dl = j.call("nativeDigestLen", h)
+    assert dl == (32, 20, 16)[algo]
+    prm = O.Params(hash_algo=algo)
+    for n in (1, 4096, 65536 + 17, 262144):
+        data = O.synth(O.SYNTH_SEED, 3000 + n % 97, 0, n).tobytes()
+        cap = j.call("nativeSlotCap", h, n)
+        arr = j.byte_array(data)
+        st, ln, dg = j.new(2, cap), j.new(2, cap), j.new(1, cap * dl)
+        cnt = j.call("nativeGetChunks", h, arr, st, ln, dg)
+        assert j.exception() is None
+        es, el, ed = O.chunk(data, prm)
+        assert cnt == len(es)
+        assert j.read(st, np.int32, cnt).tolist() == es.tolist()
+        assert j.read(ln, np.int32, cnt).tolist() == el.tolist()
+        assert j.read(dg, np.uint8, cnt * dl).tobytes() == ed.tobytes()
+        out = j.new(1, dl)
+        assert j.call("nativeGetHash", h, arr, out) == 0
+        want = (hashlib.md5 if algo == 2 else hashlib.sha256)(data).digest()[:dl]
+        assert j.read(out, np.uint8, dl).tobytes() == want
+        for a in (arr, st, ln, dg, out):
+            j.stub.stub_free(a)
+    # capacity too small for the chunk list -> IOException (getChunks' checked exception)
+    data = O.synth(O.SYNTH_SEED, 77, 0, 262144).tobytes()
+    arr = j.byte_array(data)
+    st, ln, dg = j.new(2, 2), j.new(2, 2), j.new(1, 2 * dl)
+    assert j.call("nativeGetChunks", h, arr, st, ln, dg) == -1
+    cls, msg = j.exception()
+    assert cls == "java/io/IOException" and "cap" in msg
+    j.call("nativeDestroy", h)

@@ -124,3 +124,26 @@ def test_batch_equals_single_calls_and_threads():
             assert counts[i] == len(s1)
             assert st[i, : counts[i]].tolist() == list(s1) and ln[i, : counts[i]].tolist() == list(l1)
             assert (dg[i, : counts[i]] == d1).all()
+
+
+@pytest.mark.parametrize("fx", G.fixtures(), ids=lambda f: f["name"])
+def test_fast_cpu_form_equals_reference_loop(fx):
+    """oracle/cdc_fast.c (bench.py's CPU baseline: table loop + OpenSSL digests) gives the same
+    chunks and digests as the restatement on every golden fixture."""
+    data = G.fixture_input(fx)
+    p = O.Params(**fx["params"])
+    got, exp = O.chunk_fast(data, p), O.chunk(data, p)
+    for x, y in zip(got, exp):
+        assert np.array_equal(x, y), fx["name"]
+
+
+def test_fast_cpu_form_edge_lengths_and_params():
+    for n in (0, 1, 47, 48, 49, 4095, 4096, 4097, 32767, 32768, 32769, 262144):
+        data = O.synth(O.SYNTH_SEED, 5, 3, n)
+        for p in (O.Params(), O.Params(min_len=0, max_len=100, pred_mask=0xF), O.Params(min_len=2047, pred_mask=0x7FF),
+                  O.Params(min_cmp=O.MIN_GE, hash_algo=O.MD5), O.Params(hash_algo=O.SHA256_160, window=32)):
+            got, exp = O.chunk_fast(data, p), O.chunk(data, p)
+            for x, y in zip(got, exp):
+                assert np.array_equal(x, y), (n, p)
+    z = np.zeros(262144, np.uint8)
+    assert np.array_equal(O.chunk_fast(z)[1], O.chunk(z)[1])

@@ -1,0 +1,76 @@
+"""ctypes binding of tools/libsdfs_threads.so (tools/threads_bench.c): T C threads calling the
+engine's getChunks / getHash one buffer at a time, SDFS's flush-thread pattern
+(SparseDedupFile.java:100,432; WritableCacheBuffer.java:100-104).  Bench/test infrastructure."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libsdfs_threads.so")
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("secs", ctypes.c_double), ("gibps", ctypes.c_double), ("mean_us", ctypes.c_double),
+                ("p50_us", ctypes.c_double), ("p90_us", ctypes.c_double), ("p99_us", ctypes.c_double),
+                ("max_us", ctypes.c_double), ("calls", ctypes.c_uint64), ("first_error", ctypes.c_int)]
+
+    def as_dict(self) -> dict:
+        return {k: (round(getattr(self, k), 3) if isinstance(getattr(self, k), float) else getattr(self, k))
+                for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        from sdfs_amd import _lib as engine_lib
+        engine_lib.load()  # the engine (and torch's HIP runtime) first
+        lib = ctypes.CDLL(LIB)
+        vp = ctypes.c_void_p
+        lib.sdfs_threads_getchunks.argtypes = [vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                               ctypes.c_uint32, vp, vp, vp, vp, ctypes.POINTER(Result)]
+        lib.sdfs_threads_gethash.argtypes = [vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                             ctypes.c_int, vp, ctypes.POINTER(Result)]
+        _lib = lib
+    return _lib
+
+
+def getchunks(engine, nthreads: int, data: np.ndarray, buf_len: int, total_calls: int, keep: bool = False):
+    """data: nbuf * buf_len host bytes.  Returns (Result, results) where results is
+    (counts[nbuf], starts[nbuf, cap], lens[nbuf, cap], digests[nbuf, cap, dl]) when keep."""
+    lib = load()
+    data = np.ascontiguousarray(data, np.uint8)
+    nbuf = data.size // buf_len
+    cap = engine.slot_cap(buf_len)
+    res = Result()
+    if keep:
+        counts = np.zeros(nbuf, np.uint32)
+        st = np.zeros((nbuf, cap), np.uint32)
+        ln = np.zeros((nbuf, cap), np.uint32)
+        dg = np.zeros((nbuf, cap, engine.digest_len), np.uint8)
+        ptrs = (counts.ctypes.data, st.ctypes.data, ln.ctypes.data, dg.ctypes.data)
+    else:
+        ptrs = (None, None, None, None)
+    rc = lib.sdfs_threads_getchunks(engine._h, nthreads, data.ctypes.data, nbuf, buf_len, total_calls, cap, *ptrs,
+                                    ctypes.byref(res))
+    if rc:
+        raise RuntimeError(f"threads harness failed to start its threads ({rc})")
+    return res, ((counts, st, ln, dg) if keep else None)
+
+
+def gethash(engine, nthreads: int, data: np.ndarray, buf_len: int, total_calls: int, keep: bool = False):
+    lib = load()
+    data = np.ascontiguousarray(data, np.uint8)
+    nbuf = data.size // buf_len
+    dg = np.zeros((nbuf, 32), np.uint8)
+    res = Result()
+    rc = lib.sdfs_threads_gethash(engine._h, nthreads, data.ctypes.data, nbuf, buf_len, total_calls, 1 if keep else 0,
+                                  dg.ctypes.data, ctypes.byref(res))
+    if rc:
+        raise RuntimeError(f"threads harness failed to start its threads ({rc})")
+    return res, (dg[:, :engine.digest_len] if keep else None)
