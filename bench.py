@@ -79,6 +79,18 @@ def load_traffic(name: str, params: str):
     return d[name].get("hbm_bytes_per_launch"), f"{d.get('source', '?')} (commit {d.get('commit', '?')})"
 
 
+def cpu_quota():
+    """The cgroup CPU quota (cpu.max) in CPUs, or None when there is none (on the GPU box nproc and
+    the affinity mask show the whole machine; a job's share is 16 CPUs per GPU)."""
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return round(int(q) / int(period), 2)
+    except Exception:
+        pass
+    return None
+
+
 def git_head() -> str:
     try:
         return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
@@ -167,7 +179,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-1t-secs", type=float, default=3.0, help="single-thread CPU baseline sample (0 = skip)")
     ap.add_argument("--e2e-mib", type=int, default=1024, help="host->GPU->host batch measurement size (0 = skip)")
-    ap.add_argument("--threads", default="1,8,32,128,384",
+    ap.add_argument("--threads", default="1,8,32,64,128,256",
                     help="getChunks caller-thread counts for the coalescing-queue sweep ('' = skip)")
     ap.add_argument("--min-seg-kib", type=int, default=4,
                     help="min-variable-segment-size (minLen = KiB*1024-1; 4 = the reference default)")
@@ -179,6 +191,7 @@ def main():
     ap.add_argument("--ramp-secs", type=float, default=0.3, help="untimed clock ramp before the warmup steps")
     ap.add_argument("--streams-in-flight", type=int, default=2, choices=[1, 2],
                     help="HIP streams the steps alternate on (2 = production: two batches in flight)")
+    ap.add_argument("--compare", type=int, default=1, help="also time the other streams-in-flight mode (N = 1)")
     ap.add_argument("--exchange", type=int, default=-1,
                     help="record all-gather: -1 = when N > 1, 1 = also at N = 1 (exercises the path)")
     args = ap.parse_args()
@@ -273,7 +286,7 @@ def main():
 
     # the other in-flight mode beside the headline (N = 1 only)
     other = None
-    if world == 1:
+    if world == 1 and args.compare:
         def one():
             batch.run(buffer_id_base=base_id, stream=cs.cuda_stream)
 
@@ -359,7 +372,8 @@ def main():
     if world == 1 and args.cpu_secs > 0:
         # the GPU box's CPU share is 16 cores per GPU (the host's nproc shows the whole machine)
         aff = len(os.sched_getaffinity(0))
-        th = args.cpu_threads or min(16, aff)
+        quota = cpu_quota()
+        th = args.cpu_threads or max(1, min(16 if quota is None else int(quota), aff))
         p_kw = dict(min_len=cfg.min_len, pred_mask=cfg.pred_mask)
         log(f"cpu baseline: {th} threads, ~{args.cpu_secs}s sample")
         cpu = cpu_baseline(args.cpu_secs, th, p_kw)
@@ -368,6 +382,7 @@ def main():
             cpu["one_thread"] = {"value": one["value"], "sample": one["sample"]}
         cpu["cpu_model"] = cpu_model()
         cpu["affinity_cpus"] = aff
+        cpu["cpu_quota"] = quota
     res = {
         "metric": METRIC,
         "value": round(value, 3),

@@ -143,8 +143,11 @@ int sdfs_cdc_hash_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64
  * Synchronous for the caller; concurrent callers share GPU passes (see "Threading"). */
 int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, uint32_t* starts,
                         uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count);
-/* Coalescing statistics since create: GPU passes launched and getChunks/getHash calls they served. */
+/* Coalescing statistics since create: GPU passes launched and getChunks/getHash calls they served;
+ * mean microseconds per pass spent filling (first call joined -> pass closed), waiting for the
+ * callers' copies into pinned staging, and on the device (transfers + kernels). */
 int sdfs_cdc_queue_stats(sdfs_cdc_engine* e, uint64_t* batches, uint64_t* requests);
+int sdfs_cdc_queue_timing(sdfs_cdc_engine* e, double* fill_us, double* copy_us, double* device_us);
 
 /* Batched getChunks over nbuf independent host buffers at base+offs[b], lens[b] (each chunked
  * from fresh state; SURVEY.md 0 "every call starts from a fresh state").  Per-buffer slots of

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Coalescing-queue probe: T C threads calling getChunks (tools/threads_bench.c) on one engine;
+prints rate, latency percentiles and the queue's own per-pass timeline (fill / copy / device).
+Env: THREADS (list), QI (queue in-flight depths; tuning library only when != default)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from sdfs_amd import HipVariableSha256HashEngine  # noqa: E402
+from sdfs_amd.device import DeviceBatch  # noqa: E402
+from tools import threads as T  # noqa: E402
+
+L = 262144
+nb = 1024
+e0 = HipVariableSha256HashEngine()
+b = DeviceBatch(e0, nbuf=nb, buf_len=L)
+b.fill_streams(0, 64)
+torch.cuda.synchronize()
+host = b.data.cpu().numpy()
+del b
+e0.destroy()
+for th in [int(x) for x in os.environ.get("THREADS", "1,32,128,384").split(",")]:
+    e = HipVariableSha256HashEngine()
+    T.getchunks(e, 8, host, L, 64)
+    b0 = e.queue_stats()
+    calls = max(256, th * 8)
+    r, _ = T.getchunks(e, th, host, L, calls)
+    b1 = e.queue_stats()
+    print(json.dumps({"threads": th, "qi": os.environ.get("SDFS_Q_INFLIGHT", "default"), "gibps": round(r.gibps, 3),
+                      "p50_us": round(r.p50_us), "p99_us": round(r.p99_us), "calls_per_pass":
+                      round((b1[1] - b0[1]) / max(b1[0] - b0[0], 1), 1), **e.queue_timing()}), flush=True)
+    e.destroy()

@@ -93,6 +93,7 @@ SIGNATURES = {
                                                   ctypes.c_uint64, _P(DevOut), _vp]),
     "sdfs_cdc_stream_sync": (ctypes.c_int, [_vp]),
     "sdfs_cdc_queue_stats": (ctypes.c_int, [_vp, _u64p, _u64p]),
+    "sdfs_cdc_queue_timing": (ctypes.c_int, [_vp, _P(ctypes.c_double), _P(ctypes.c_double), _P(ctypes.c_double)]),
     "sdfs_cdc_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "sdfs_cdc_set_timing_mask": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32]),
     "sdfs_cdc_kernel_times": (ctypes.c_int, [_vp, _P(ctypes.c_char_p), _P(ctypes.c_float), ctypes.c_int]),

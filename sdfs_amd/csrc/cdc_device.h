@@ -416,9 +416,9 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.tab_image);
         uint4* dst = reinterpret_cast<uint4*>(tab);
-        for (int i = threadIdx.x; i < CFG::kLds / 16; i += kScanThreads) dst[i] = src[i];
+        for (int i = threadIdx.x; i < CFG::kLds / 16; i += blockDim.x) dst[i] = src[i];
         if constexpr (CFG::kFuse != 0)
-            for (uint32_t i = threadIdx.x; i < kMaxBins; i += kScanThreads) lhist[i] = 0;
+            for (uint32_t i = threadIdx.x; i < kMaxBins; i += blockDim.x) lhist[i] = 0;
     }
     __syncthreads();
 
@@ -426,7 +426,9 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
     const uint32_t c8 = (lane & (C - 1)) << 3;
     const uint32_t push_base = CFG::kPushOff | c8;
     const uint64_t total = a.uniform_len ? a.total_segs : a.seg_prefix[a.nbuf];
-    const uint64_t per_iter = (uint64_t)kScanThreads * NCH;
+    // workgroups of 64..1024 threads (a multiple of 64: a wave never straddles two buffers of the
+    // fused walk); small batches launch narrow workgroups so their waves do not share SIMDs
+    const uint64_t per_iter = (uint64_t)blockDim.x * NCH;
 
     for (uint64_t base = (uint64_t)blockIdx.x * per_iter; base < total; base += (uint64_t)gridDim.x * per_iter) {
         uint64_t start[NCH], end[NCH];
@@ -435,7 +437,7 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
         uint32_t maxblk = 0;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
-            const uint64_t seg = base + (uint64_t)c * kScanThreads + threadIdx.x;
+            const uint64_t seg = base + (uint64_t)c * blockDim.x + threadIdx.x;
             start[c] = end[c] = 0;
             nblk[c] = 0;
             first[c] = true;
@@ -602,7 +604,7 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
     if constexpr (CFG::kFuse != 0) {
         if (a.fuse_resolve) {
             __syncthreads();
-            for (uint32_t i = threadIdx.x; i < a.res.nbins; i += kScanThreads)
+            for (uint32_t i = threadIdx.x; i < a.res.nbins; i += blockDim.x)
                 if (lhist[i]) atomicAdd(&a.res.hist[i], lhist[i]);
         }
     }

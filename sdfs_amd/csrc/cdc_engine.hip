@@ -137,7 +137,9 @@ constexpr int kEvPerRun = 2 * 8;
 // recorded after its previous run (cross-stream wait, no host sync).
 constexpr uint32_t kSmall = 2 * kMaxBins + 8;  // hist | cursor | overflow, total, wave_ctr ..
 constexpr int kRing = 3;
-
+constexpr int kQueueInflight = 4;  // coalescing-queue lanes: batches on the device at once, one stream each
+                                   // (GPU_MAX_HW_QUEUES is 4: more streams would share hardware queues)
+constexpr int kQueueSlots = 8;
 struct Workspace {
     DevBuf<uint32_t> bitmap;
     DevBuf<uint64_t> seg_prefix;
@@ -176,9 +178,13 @@ struct HostSlot {
     uint32_t b0 = 0, n = 0, dcap = 0;
 };
 
-// Device state of one coalescing-queue slot (host_queue.h): the batch's device copy, its outputs
-// and the pinned result image the callers read:
+// Device state of one coalescing-queue slot (host_queue.h): the batch's device copy, and its
+// result image, written by the kernels in place on the device (dimg) and copied to pinned host
+// memory (pin_out) in ONE transfer once the kernels are done:
 //   counts[n] | starts[n*dcap] | lens[n*dcap] | flags[16] | digests[n*dcap*32] | hash digests[nh*32]
+// The copy back is issued by the completer after the kernels finished, not queued behind them at
+// launch: copies of every stream go through the same DMA queue in order, so a device->host copy
+// waiting on one batch's kernels would hold up the next batch's host->device copy.
 struct QSlotDev {
     uint8_t* pin_meta = nullptr;  // chunk offs u64[max_reqs] | lens u32 | hash offs u64 | lens u32
     size_t pin_meta_n = 0;
@@ -187,12 +193,14 @@ struct QSlotDev {
     DevBuf<uint8_t> data;
     DevBuf<uint64_t> meta64;  // chunk offs | hash offs
     DevBuf<uint32_t> meta32;  // chunk lens | hash lens
-    DevBuf<uint32_t> counts, starts, clens, total;
-    DevBuf<uint8_t> digests, h_digests;
-    hipEvent_t done = nullptr;
+    DevBuf<uint32_t> total;
+    DevBuf<uint8_t> dimg;     // device result image (pin_out's layout)
+    Workspace ws;  // the slot's own pipeline scratch (a slot is reused only after its batch completed)
+    hipEvent_t kdone = nullptr;  // kernels of the batch done
+    hipStream_t st = nullptr;    // the lane stream it runs on
     // layout of the batch in flight (read by the callers)
     uint32_t n = 0, nh = 0, dcap = 0;
-    uint64_t digests_at = 0, hdig_at = 0;
+    uint64_t digests_at = 0, hdig_at = 0, img_bytes = 0;
     std::string err;  // message of a failed launch/wait (set on the queue's threads)
 };
 
@@ -235,8 +243,7 @@ struct sdfs_cdc_engine {
     int copy_threads = 8;
     std::unique_ptr<CopyPool> pool;
     // coalescing queue for concurrent single-buffer callers
-    hipStream_t qs[2] = {nullptr, nullptr};
-    uint32_t q_next = 0;
+    hipStream_t qs[kQueueInflight] = {};
     std::unique_ptr<QueueBackend> qb;
     std::unique_ptr<CoalescingQueue<QueueBackend>> q;
     std::mutex q_init;
@@ -282,10 +289,10 @@ struct WsNeed {
     uint64_t bitmap_words = 0, seg_prefix = 0, rec_base = 0, tasks = 0, spec_starts = 0, spec_items = 0, x_scratch = 0;
 };
 
-// Next workspace of the ring, sized for `nd`, ordered behind its previous use on `s`.  Caller
-// holds e->mu and has set the device.
-int ws_acquire(sdfs_cdc_engine* e, const WsNeed& nd, hipStream_t s, Workspace** out) {
-    Workspace* w = &e->ws[e->ws_next++ % kRing];
+// Next workspace of the ring (or `own`, a queue slot's), sized for `nd`, ordered behind its
+// previous use on `s`.  Caller holds e->mu and has set the device.
+int ws_acquire(sdfs_cdc_engine* e, const WsNeed& nd, hipStream_t s, Workspace** out, Workspace* own = nullptr) {
+    Workspace* w = own ? own : &e->ws[e->ws_next++ % kRing];
     const bool fits = w->bitmap.fits(nd.bitmap_words) && w->small.fits(kSmall + 8) &&
                       w->rec_base.fits(nd.rec_base) && w->tasks.fits(nd.tasks) &&
                       (!nd.seg_prefix || w->seg_prefix.fits(nd.seg_prefix)) &&
@@ -355,7 +362,7 @@ WsNeed pipeline_need(const sdfs_cdc_engine* e, uint64_t data_bytes, uint32_t nbu
 int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
                  const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
                  const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, uint32_t sec_len, uint32_t nsec,
-                 uint32_t spec_cap) {
+                 uint32_t spec_cap, uint32_t* ovf_to = nullptr) {
     e->run = nullptr;
     if (e->timing_slots > 0) {
         e->run = &e->ev_runs[e->runs_recorded % e->timing_slots];
@@ -375,6 +382,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     {
         const int t = t_begin(e, K_PREP, s);
         HIP_TRY(hipMemsetAsync(w->small.p, 0, (kSmall + 8) * sizeof(uint32_t), s));
+        if (ovf_to) HIP_TRY(hipMemsetAsync(ovf_to, 0, sizeof(uint32_t), s));
         if (!uniform_len) HIP_TRY(launch_seg_prefix(d_lens, nbuf, e->seg_len, w->seg_prefix.p, s));
         t_end(e, t, s);
     }
@@ -418,7 +426,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     ra.starts = out->starts;
     ra.clens = out->lens;
     ra.hist = hist;
-    ra.overflow = w->overflow();
+    ra.overflow = ovf_to ? ovf_to : w->overflow();
     ra.max_buf_len = uniform_len ? uniform_len : max_buf_len;
     ra.sec_len = sec_len;
     if (sec_len) {
@@ -433,13 +441,20 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
                        (uint64_t)uniform_len == 64ull * e->seg_len && e->seg_len < 0xFFFFu;
     sa.fuse_resolve = fused ? 1u : 0u;
     sa.res = ra;
-    const uint64_t per_block = (uint64_t)kScanThreads * e->scan_info.chains;
+    // One workgroup per CU (the LDS tables); a batch too small to give every CU 1024 threads
+    // (fewer than ~4096 write buffers, e.g. the coalescing queue's) launches narrower
+    // workgroups, so its waves run one per SIMD instead of four on a few CUs.
+    const uint64_t max_wgs = (uint64_t)e->num_cus * e->scan_info.wg_per_cu;
+    const uint64_t lanes = (seg_bound + e->scan_info.chains - 1) / e->scan_info.chains;
+    uint64_t block = (lanes + max_wgs - 1) / max_wgs;
+    block = std::min<uint64_t>(std::max<uint64_t>((block + 255) / 256 * 256, 256), kScanThreads);
+    const uint64_t per_block = block * e->scan_info.chains;
     uint64_t grid = (seg_bound + per_block - 1) / per_block;
-    grid = std::min<uint64_t>(grid, (uint64_t)e->num_cus * e->scan_info.wg_per_cu);
+    grid = std::min<uint64_t>(grid, max_wgs);
     grid = std::max<uint64_t>(grid, 1);
     {
         const int t = t_begin(e, K_SCAN, s);
-        HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, s));
+        HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, (int)block, s));
         t_end(e, t, s);
     }
     if (!fused) {
@@ -508,7 +523,8 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
 // use) when ovf_dev != NULL.  Caller holds e->mu.
 int device_run(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
                const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
-               const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, const uint32_t** ovf_dev) {
+               const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, const uint32_t** ovf_dev,
+               Workspace* own = nullptr, uint32_t* ovf_to = nullptr) {
     if (!out || !out->counts || !out->starts || !out->lens || !out->digests || !out->total)
         return fail(SDFS_CDC_EINVAL, "incomplete sdfs_cdc_dev_out");
     if (uniform_len && (uniform_len & 63)) return fail(SDFS_CDC_EINVAL, "uniform_len must be a multiple of 64");
@@ -520,10 +536,10 @@ int device_run(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, c
     uint32_t sec_len, nsec, spec_cap;
     const WsNeed nd = pipeline_need(e, data_bytes, nbuf, uniform_len, out->cap, max_buf_len, &sec_len, &nsec, &spec_cap);
     Workspace* w = nullptr;
-    int rc = ws_acquire(e, nd, s, &w);
+    int rc = ws_acquire(e, nd, s, &w, own);
     if (rc) return rc;
     rc = run_pipeline(e, w, d_data, data_bytes, d_offs, d_lens, nbuf, uniform_len, buffer_id_base, out, s, max_buf_len,
-                      sec_len, nsec, spec_cap);
+                      sec_len, nsec, spec_cap, ovf_to);
     const int rr = ws_release(w, s);  // even after a failed enqueue: what was enqueued completes first
     if (ovf_dev) *ovf_dev = w->overflow();
     return rc ? rc : rr;
@@ -531,13 +547,14 @@ int device_run(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, c
 
 // Fingerprints of n extents on workspace scratch (getHash in bulk).  Caller holds e->mu.
 int hash_extents(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
-                 const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, hipStream_t s) {
+                 const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, hipStream_t s,
+                 Workspace* own = nullptr) {
     if (n_max == 0) return SDFS_CDC_OK;
     if (n_max > 0xFFFFFFFFull) return fail(SDFS_CDC_EINVAL, "more than 2^32 extents");
     WsNeed nd;
     nd.x_scratch = kExtentScratchWords + 2 * n_max;
     Workspace* w = nullptr;
-    int rc = ws_acquire(e, nd, s, &w);
+    int rc = ws_acquire(e, nd, s, &w, own);
     if (rc) return rc;
     uint32_t* sc = w->x_scratch.p;
     ExtentArgs xa{d_lens, d_count, n_max, sc + kExtentScratchWords, sc + kExtentScratchWords + n_max,
@@ -786,37 +803,61 @@ struct QueueBackend {
     uint64_t slot_bytes;
     uint32_t max_reqs;
 
+    uint64_t out_entries;  // chunk slots of a slot's result image: sum over its requests of dcap
+
+    // Everything a slot needs is allocated here, once: growing a device buffer later would free
+    // the old one, and hipFree waits for the whole device (every batch in flight).
     int prepare(QSlot& s) {
         HIP_TRY(hipSetDevice(e->prm.device));
         auto* d = new QSlotDev();
         s.dev = d;
         int rc = pinned_ensure(&s.in, &s.cap, slot_bytes);
         if (!rc) rc = pinned_ensure(&d->pin_meta, &d->pin_meta_n, (size_t)max_reqs * 24 + 64);
+        if (!rc) rc = pinned_ensure(&d->pin_out, &d->pin_out_n, image_bytes(max_reqs, out_entries, max_reqs));
         if (rc) return rc;
         s.cap = slot_bytes;
         HIP_TRY(d->data.ensure(slot_bytes));
         HIP_TRY(d->meta64.ensure(2ull * max_reqs));
         HIP_TRY(d->meta32.ensure(2ull * max_reqs));
         HIP_TRY(d->total.ensure(1));
-        HIP_TRY(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
+        HIP_TRY(d->dimg.ensure(image_bytes(max_reqs, out_entries, max_reqs)));
+        Workspace& w = d->ws;
+        HIP_TRY(w.bitmap.ensure(slot_bytes / 32 + 2));
+        HIP_TRY(w.small.ensure(kSmall + 8));
+        HIP_TRY(w.rec_base.ensure(max_reqs));
+        HIP_TRY(w.tasks.ensure(out_entries));
+        HIP_TRY(w.seg_prefix.ensure(max_reqs + 1ull));
+        HIP_TRY(w.x_scratch.ensure(kExtentScratchWords + 2ull * max_reqs));
+        HIP_TRY(hipEventCreateWithFlags(&d->kdone, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&d->ws.free_ev, hipEventDisableTiming));
         return SDFS_CDC_OK;
+    }
+
+    // result image: counts[n] | starts[n*dcap] | lens[n*dcap] | flags[16] | digests | hash digests
+    static uint64_t image_bytes(uint64_t n, uint64_t nout, uint64_t nh) {
+        return ((n * 4 + nout * 8 + 64 + 15) & ~15ull) + nout * 32 + nh * 32 + 64;
+    }
+
+    bool admits(const QSlot& s, const QReq& r) {
+        if (r.kind != QReq::kChunks) return true;
+        const uint64_t dcap = slot_cap_for(e->prm, std::max<uint64_t>(std::max<uint64_t>(s.max_chunk_len, r.len), 1));
+        return (s.chunks.size() + 1) * dcap <= out_entries;
     }
 
     void release(QSlot& s) {
         auto* d = static_cast<QSlotDev*>(s.dev);
         (void)hipSetDevice(e->prm.device);
         if (d) {
-            if (d->done) {
-                (void)hipEventSynchronize(d->done);
-                (void)hipEventDestroy(d->done);
-            }
+            if (d->st) (void)hipStreamSynchronize(d->st);
+            if (d->kdone) (void)hipEventDestroy(d->kdone);
             if (d->pin_meta) (void)hipHostFree(d->pin_meta);
             if (d->pin_out) (void)hipHostFree(d->pin_out);
-            for (auto* b : {&d->counts, &d->starts, &d->clens, &d->total, &d->meta32}) b->release();
+            for (auto* b : {&d->total, &d->meta32}) b->release();
+            d->dimg.release();
+            d->ws.release_all();
+            if (d->ws.free_ev) (void)hipEventDestroy(d->ws.free_ev);
             d->meta64.release();
             d->data.release();
-            d->digests.release();
-            d->h_digests.release();
             delete d;
         }
         if (s.in) (void)hipHostFree(s.in);
@@ -826,11 +867,12 @@ struct QueueBackend {
     }
 
     // Runs on the queue's dispatcher thread: the error message goes with the slot to the callers.
-    int launch(QSlot& s) {
+    int launch(QSlot& s, int lane) {
         std::lock_guard<std::mutex> lk(e->mu);
         auto* d = static_cast<QSlotDev*>(s.dev);
         d->err.clear();
-        hipStream_t st = e->qs[e->q_next++ & 1];
+        hipStream_t st = e->qs[lane % kQueueInflight];
+        d->st = st;
         const int rc = launch_impl(s, d, st);
         if (rc) {
             d->err = g_last_error;
@@ -847,13 +889,15 @@ struct QueueBackend {
         const uint32_t n = (uint32_t)s.chunks.size(), nh = (uint32_t)s.hashes.size();
         const uint32_t dcap = n ? slot_cap_for(e->prm, std::max<uint64_t>(s.max_chunk_len, 1)) : 0;
         const uint64_t nout = (uint64_t)n * dcap;
+        if (nout > out_entries || n > max_reqs || nh > max_reqs)
+            return fail(SDFS_CDC_EHIP, "internal: queue slot over its result capacity");
         d->n = n;
         d->nh = nh;
         d->dcap = dcap;
         d->digests_at = (n * 4ull + nout * 8 + 64 + 15) & ~15ull;
         d->hdig_at = d->digests_at + nout * 32;
-        int rc = pinned_ensure(&d->pin_out, &d->pin_out_n, d->hdig_at + nh * 32ull + 64);
-        if (rc) return rc;
+        d->img_bytes = d->hdig_at + 32ull * nh;
+        int rc = SDFS_CDC_OK;
         uint64_t* m64 = reinterpret_cast<uint64_t*>(d->pin_meta);
         uint32_t* m32 = reinterpret_cast<uint32_t*>(m64 + 2ull * max_reqs);
         for (uint32_t i = 0; i < n; i++) {
@@ -868,44 +912,29 @@ struct QueueBackend {
         if (s.hi < s.cap) HIP_TRY(hipMemcpyAsync(d->data.p + s.hi, s.in + s.hi, s.cap - s.hi, hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemcpyAsync(d->meta64.p, m64, 16ull * max_reqs, hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemcpyAsync(d->meta32.p, m32, 8ull * max_reqs, hipMemcpyHostToDevice, st));
-        uint32_t* pc = reinterpret_cast<uint32_t*>(d->pin_out);
-        uint32_t* ps = pc + n;
-        uint32_t* pl = ps + nout;
-        uint32_t* pflag = pl + nout;
-        pflag[0] = 0;
+        uint32_t* dc = reinterpret_cast<uint32_t*>(d->dimg.p);
+        uint32_t* dflag = dc + n + 2 * nout;
         if (n) {
-            HIP_TRY(d->counts.ensure(n));
-            HIP_TRY(d->starts.ensure(nout));
-            HIP_TRY(d->clens.ensure(nout));
-            HIP_TRY(d->digests.ensure(nout * 32));
             sdfs_cdc_dev_out out{};
-            out.counts = d->counts.p;
-            out.starts = d->starts.p;
-            out.lens = d->clens.p;
-            out.digests = d->digests.p;
+            out.counts = dc;
+            out.starts = dc + n;
+            out.lens = dc + n + nout;
+            out.digests = d->dimg.p + d->digests_at;
             out.cap = dcap;
             out.total = d->total.p;
             // every CHUNK_LENGTH flush buffer (the common case) takes the uniform layout and the
             // fused cut walk; mixed lengths (write-accelerator runs) the ragged one
             const uint32_t ul = (s.uniform_len && (s.uniform_len & 63) == 0) ? s.uniform_len : 0;
-            const uint32_t* ovf = nullptr;
             rc = device_run(e, d->data.p, s.lo, ul ? nullptr : d->meta64.p, ul ? nullptr : d->meta32.p, n, ul, 0,
-                            &out, st, s.max_chunk_len, &ovf);
+                            &out, st, s.max_chunk_len, nullptr, &d->ws, dflag);
             if (rc) return rc;
-            HIP_TRY(hipMemcpyAsync(pc, out.counts, n * 4ull, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipMemcpyAsync(ps, out.starts, nout * 4, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipMemcpyAsync(pl, out.lens, nout * 4, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipMemcpyAsync(pflag, ovf, 4, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipMemcpyAsync(d->pin_out + d->digests_at, out.digests, nout * 32, hipMemcpyDeviceToHost, st));
         }
         if (nh) {
-            HIP_TRY(d->h_digests.ensure(32ull * nh));
             rc = hash_extents(e, d->data.p, d->meta64.p + max_reqs, d->meta32.p + max_reqs, nullptr, nh,
-                              d->h_digests.p, st);
+                              d->dimg.p + d->hdig_at, st, &d->ws);
             if (rc) return rc;
-            HIP_TRY(hipMemcpyAsync(d->pin_out + d->hdig_at, d->h_digests.p, 32ull * nh, hipMemcpyDeviceToHost, st));
         }
-        HIP_TRY(hipEventRecord(d->done, st));
+        HIP_TRY(hipEventRecord(d->kdone, st));
         return SDFS_CDC_OK;
     }
 
@@ -917,9 +946,13 @@ struct QueueBackend {
         return rc;
     }
 
+    // Kernels done -> one copy of the result image -> done.  The lane's stream carries no other
+    // batch meanwhile (one batch per lane in flight).
     int wait_impl(QSlotDev* d) {
         HIP_TRY(hipSetDevice(e->prm.device));
-        HIP_TRY(hipEventSynchronize(d->done));
+        HIP_TRY(hipEventSynchronize(d->kdone));
+        HIP_TRY(hipMemcpyAsync(d->pin_out, d->dimg.p, d->img_bytes, hipMemcpyDeviceToHost, d->st));
+        HIP_TRY(hipStreamSynchronize(d->st));
         if (d->n) {
             const uint32_t* pflag = reinterpret_cast<const uint32_t*>(d->pin_out) + d->n + 2ull * d->n * d->dcap;
             if (*pflag) return fail(SDFS_CDC_EHIP, "internal: chunk slot overflow");
@@ -930,15 +963,23 @@ struct QueueBackend {
 
 namespace {
 
-// Starts the queue on first use (slot staging: 4 x CHUNK_LENGTH, at least 64 MiB, at most 512 MiB).
+// Starts the queue on first use.  Slot staging: 2 x CHUNK_LENGTH, at least 32 MiB (128 flush
+// buffers of 256 KiB; 40 MiB backup buffers get 80 MiB slots), at most 512 MiB.
 bool queue_ready(sdfs_cdc_engine* e) {
     std::lock_guard<std::mutex> lk(e->q_init);
     if (e->q_state) return e->q_state > 0;
-    const uint64_t slot = std::min<uint64_t>(std::max<uint64_t>(64ull << 20, 4ull * e->prm.chunk_length), 512ull << 20);
-    e->qb.reset(new QueueBackend{e, slot, 1024});
+    const uint64_t slot = std::min<uint64_t>(std::max<uint64_t>(32ull << 20, 2ull * e->prm.chunk_length), 512ull << 20);
+    // result image: room for every 64-byte-aligned request's worst-case chunk list at the
+    // shortest chunk length, plus two slots of tail per request
+    const uint64_t shortest = std::max<uint64_t>(1, std::min<uint64_t>(e->first_off + 1, e->prm.max_len));
+    e->qb.reset(new QueueBackend{e, slot, 1024, slot / shortest + 2ull * 1024});
     CoalescingQueue<QueueBackend>::Config c;
-    c.nslots = 4;
-    c.max_inflight = 2;
+    c.nslots = kQueueSlots;
+    c.lanes = kQueueInflight;
+#ifdef SDFS_TUNING
+    if (const char* v = getenv("SDFS_Q_INFLIGHT")) c.lanes = std::max(1, std::min(atoi(v), kQueueInflight));
+    if (const char* v = getenv("SDFS_Q_LINGER_US")) c.linger_us = (uint32_t)atoi(v);
+#endif
     c.max_reqs = 1024;
     c.max_req_bytes = slot / 2;
     e->q.reset(new CoalescingQueue<QueueBackend>(*e->qb, c));
@@ -1015,9 +1056,8 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     while ((maxblocks >> e->bin_shift) >= (uint32_t)kMaxBins) e->bin_shift++;
     e->nbins = (maxblocks >> e->bin_shift) + 1;
     bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->qs[0], hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->qs[1], hipStreamNonBlocking) == hipSuccess;
+              hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) == hipSuccess;
+    for (auto& q : e->qs) ok = ok && hipStreamCreateWithFlags(&q, hipStreamNonBlocking) == hipSuccess;
     for (auto& sl : e->hs)
         ok = ok && hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
@@ -1058,7 +1098,9 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
     {
         std::lock_guard<std::mutex> lk(e->mu);
         (void)hipSetDevice(e->prm.device);
-        for (hipStream_t s : {e->stream, e->s_h2d, e->qs[0], e->qs[1]})
+        for (hipStream_t s : {e->stream, e->s_h2d})
+            if (s) (void)hipStreamSynchronize(s);
+        for (hipStream_t s : e->qs)
             if (s) (void)hipStreamSynchronize(s);
         e->tab_image.release();
         e->zero_page.release();
@@ -1089,7 +1131,9 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
         for (auto& run : e->ev_runs)
             for (auto& ev : run.ev)
                 if (ev) (void)hipEventDestroy(ev);
-        for (hipStream_t s : {e->stream, e->s_h2d, e->qs[0], e->qs[1]})
+        for (hipStream_t s : {e->stream, e->s_h2d})
+            if (s) (void)hipStreamDestroy(s);
+        for (hipStream_t s : e->qs)
             if (s) (void)hipStreamDestroy(s);
     }
     delete e;
@@ -1247,6 +1291,19 @@ int sdfs_cdc_queue_stats(sdfs_cdc_engine* e, uint64_t* batches, uint64_t* reques
     std::lock_guard<std::mutex> lk(e->q_init);
     if (batches) *batches = e->q ? e->q->batches() : 0;
     if (requests) *requests = e->q ? e->q->requests() : 0;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_queue_timing(sdfs_cdc_engine* e, double* fill_us, double* copy_us, double* device_us) {
+    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+    std::lock_guard<std::mutex> lk(e->q_init);
+    if (e->q) {
+        e->q->timing(fill_us, copy_us, device_us);
+    } else {
+        if (fill_us) *fill_us = 0;
+        if (copy_us) *copy_us = 0;
+        if (device_us) *device_us = 0;
+    }
     return SDFS_CDC_OK;
 }
 

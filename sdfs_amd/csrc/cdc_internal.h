@@ -14,7 +14,7 @@ namespace sdfs {
 //             C = 16 -> (e << 8) | 0x80 | (c << 3) (interleaved with pop in 256-byte rows).
 constexpr int scan_lds_bytes(int copies) { return 2 * 256 * copies * 8; }
 
-constexpr int kScanThreads = 1024;
+constexpr int kScanThreads = 1024;  // widest scan workgroup (one per CU: the tables fill 128 KiB of LDS)
 
 struct ScanVariantInfo {
     int copies;      // table copies (image layout)
@@ -151,7 +151,8 @@ inline uint64_t splitmix64_host(uint64_t x) {
 // kernel launchers (cdc_kernels.hip); all asynchronous on `stream`
 hipError_t launch_seg_prefix(const uint32_t* lens, uint32_t nbuf, uint32_t seg_len, uint64_t* seg_prefix,
                              hipStream_t stream);
-hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t stream);
+hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, int block,
+                       hipStream_t stream);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);
@@ -164,7 +165,8 @@ bool scan_window_supported(int window);
 #ifdef SDFS_TUNING
 // measurement-only variants (cdc_sweep.hip; tuning library only)
 ScanVariantInfo scan_variant_info_sweep(int variant);
-hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t stream);
+hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int variant, int grid, int block,
+                             hipStream_t stream);
 hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);
 #endif
 

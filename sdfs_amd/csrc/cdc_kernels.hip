@@ -46,27 +46,27 @@ bool scan_window_supported(int window) {
 }
 
 template <int W, class CFG>
-static hipError_t launch_scan_wc(const ScanArgs& a, bool pred64, int grid, hipStream_t s) {
+static hipError_t launch_scan_wc(const ScanArgs& a, bool pred64, int grid, int block, hipStream_t s) {
     if (pred64)
-        hipLaunchKernelGGL((cdc_scan_kernel<W, true, CFG>), dim3(grid), dim3(kScanThreads), 0, s, a);
+        hipLaunchKernelGGL((cdc_scan_kernel<W, true, CFG>), dim3(grid), dim3(block), 0, s, a);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<W, false, CFG>), dim3(grid), dim3(kScanThreads), 0, s, a);
+        hipLaunchKernelGGL((cdc_scan_kernel<W, false, CFG>), dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t s) {
+hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, int block, hipStream_t s) {
     if (variant != 0) {
 #ifdef SDFS_TUNING
-        return launch_scan_sweep(a, window, pred64, variant, grid, s);
+        return launch_scan_sweep(a, window, pred64, variant, grid, block, s);
 #else
         return hipErrorInvalidValue;
 #endif
     }
     switch (window) {
-    case 16: return launch_scan_wc<16, ScanProd>(a, pred64, grid, s);
-    case 32: return launch_scan_wc<32, ScanProd>(a, pred64, grid, s);
-    case 48: return launch_scan_wc<48, ScanProd>(a, pred64, grid, s);
-    case 64: return launch_scan_wc<64, ScanProd>(a, pred64, grid, s);
+    case 16: return launch_scan_wc<16, ScanProd>(a, pred64, grid, block, s);
+    case 32: return launch_scan_wc<32, ScanProd>(a, pred64, grid, block, s);
+    case 48: return launch_scan_wc<48, ScanProd>(a, pred64, grid, block, s);
+    case 64: return launch_scan_wc<64, ScanProd>(a, pred64, grid, block, s);
     default: return hipErrorInvalidValue;
     }
 }

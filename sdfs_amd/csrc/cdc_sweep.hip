@@ -69,19 +69,19 @@ ScanVariantInfo scan_variant_info_sweep(int v) {
 }
 
 template <class T>
-static hipError_t sweep_launch(const ScanArgs& a, bool pred64, int grid, hipStream_t s) {
+static hipError_t sweep_launch(const ScanArgs& a, bool pred64, int grid, int block, hipStream_t s) {
     if (pred64)
-        hipLaunchKernelGGL((cdc_scan_kernel<48, true, T>), dim3(grid), dim3(kScanThreads), 0, s, a);
+        hipLaunchKernelGGL((cdc_scan_kernel<48, true, T>), dim3(grid), dim3(block), 0, s, a);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<48, false, T>), dim3(grid), dim3(kScanThreads), 0, s, a);
+        hipLaunchKernelGGL((cdc_scan_kernel<48, false, T>), dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int variant, int grid, hipStream_t s) {
+hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int variant, int grid, int block, hipStream_t s) {
     if (window != 48) return hipErrorInvalidValue;  // variants are built for the reference window only
     switch (variant) {
 #define SWEEP_CASE(id, T) \
-    case id: return sweep_launch<T>(a, pred64, grid, s);
+    case id: return sweep_launch<T>(a, pred64, grid, block, s);
     SWEEP_CASE(1, ScanV1) SWEEP_CASE(2, ScanV2) SWEEP_CASE(3, ScanV3) SWEEP_CASE(4, ScanV4)
     SWEEP_CASE(5, ScanV5) SWEEP_CASE(6, ScanV6) SWEEP_CASE(7, ScanV7) SWEEP_CASE(8, ScanV8)
     SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16)

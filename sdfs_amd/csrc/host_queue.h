@@ -8,24 +8,25 @@
 // getChunks from the same pool, WritableCacheBuffer.java:640-643).  A GPU round trip per
 // 256 KiB buffer would leave the device idle, so concurrent calls are coalesced:
 //
-//   caller thread                          dispatcher thread          completer thread
+//   caller thread                          dispatcher thread          completer thread (per lane)
 //   reserve space in the OPEN slot  ──┐
-//   copy its bytes into pinned staging │    OPEN slot has requests
-//   (in parallel with other callers)   └─►  and < max_inflight in
-//   wait for its request's `done`           flight: CLOSE it, wait
-//                                           for the copies, launch ─► wait for the device,
+//   copy its bytes into pinned staging │    OPEN slot ready and a
+//   (in parallel with other callers)   └─►  device lane idle: CLOSE
+//   wait for its request's `done`           it, wait for the copies,
+//                                           launch on that lane ────► wait for the device,
 //   copy its results out of the slot ◄───────────────────────────────  mark every request done
 //   last reader frees the slot
 //
 // The batch size adapts to the load: an idle engine launches a request at once; under load the
-// OPEN slot fills while `max_inflight` batches are on the device.  Requests that do not fit a
-// slot bypass the queue (the caller handles them directly).
+// OPEN slot fills while the lanes are busy (policy below).  Requests that do not fit a slot
+// bypass the queue (the caller handles them directly).
 //
 // CopyPool: a small persistent thread pool for host memcpy into pinned staging
 // (sdfs_cdc_get_chunks_batch from pageable memory).
 #pragma once
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -142,10 +143,12 @@ struct QSlot {
     std::vector<QReq*> chunks, hashes;
     uint32_t uniform_len = 0;  // every chunk request has this length (0 = mixed)
     uint64_t max_chunk_len = 0;
+    bool full = false;  // cannot take another request of the largest admitted size
     int copying = 0;  // callers still copying their bytes in
     int readers = 0;  // callers yet to copy their results out
     int status = 0;
     uint64_t seq = 0;
+    std::chrono::steady_clock::time_point t_open, t_close, t_launch, t_done;  // batch timeline
     void* dev = nullptr;  // backend state of this slot
     size_t nreq() const { return chunks.size() + hashes.size(); }
 };
@@ -159,21 +162,33 @@ constexpr int kQueueTooBig = -1001;   // the request exceeds the per-request lim
 // Backend concept:
 //   int  prepare(QSlot&)   allocate s.in / s.cap and s.dev (called once per slot, queue lock held;
 //                          on failure the queue calls release on every slot)
-//   int  launch(QSlot&)    enqueue transfer + compute of a CLOSED slot (dispatcher thread)
-//   int  wait(QSlot&)      block until that work completed (completer thread)
+//   bool admits(const QSlot&, const QReq&)  whether the slot's result image has room for one more
+//                          request (queue lock held; must be true for an empty slot)
+//   int  launch(QSlot&, int lane)  enqueue transfer + compute of a CLOSED slot on device lane
+//                          `lane` (one stream per lane; dispatcher thread)
+//   int  wait(QSlot&)      block until that work completed (the lane's completer thread)
 //   void release(QSlot&)   free what prepare allocated
 // launch and wait run without the queue lock.
+//
+// Dispatch policy.  A batch costs the device about the same time whatever its size (its
+// longest chunk's serial SHA-256 chain sets it), so batches should be as large as the callers
+// allow, but no caller should wait long: the dispatcher launches the OPEN slot onto an idle lane
+// when nothing is in flight, or when it holds its share of the callers (active callers /
+// lanes), or when it is full, or when its first request has waited `linger_us`.
 template <class Backend>
 class CoalescingQueue {
   public:
     struct Config {
-        int nslots = 4;           // staging slots (one open, up to max_inflight in flight, readers)
-        int max_inflight = 2;     // batches on the device at once
-        uint32_t max_reqs = 1024; // requests per slot (the backend sizes its result image for this)
+        int nslots = 8;            // staging slots (one open, up to `lanes` in flight, readers)
+        int lanes = 4;             // batches on the device at once, one stream each
+        uint32_t max_reqs = 1024;  // requests per slot (the backend sizes its result image for this)
         uint64_t max_req_bytes = 0;  // larger requests bypass the queue (0 = cap / 2)
+        uint32_t linger_us = 250;  // longest a request waits for company while a batch is in flight
     };
 
-    CoalescingQueue(Backend& b, Config c) : b_(b), c_(c), slots_(c.nslots) {}
+    CoalescingQueue(Backend& b, Config c)
+        : b_(b), c_(c), slots_(c.nslots), done_cv_(c.nslots), flight_(c.lanes), comp_cv_(c.lanes),
+          lane_busy_(c.lanes, 0) {}
     ~CoalescingQueue() { shutdown(); }
     CoalescingQueue(const CoalescingQueue&) = delete;
     CoalescingQueue& operator=(const CoalescingQueue&) = delete;
@@ -200,7 +215,7 @@ class CoalescingQueue {
         prepared_ = true;
         stop_ = false;
         disp_ = std::thread([this] { dispatcher(); });
-        comp_ = std::thread([this] { completer(); });
+        for (int l = 0; l < c_.lanes; l++) comp_.emplace_back([this, l] { completer(l); });
         return 0;
     }
 
@@ -213,9 +228,11 @@ class CoalescingQueue {
             stop_ = true;
         }
         cv_disp_.notify_all();
-        cv_comp_.notify_all();
+        for (auto& cv : comp_cv_) cv.notify_all();
         if (disp_.joinable()) disp_.join();
-        if (comp_.joinable()) comp_.join();
+        for (auto& t : comp_)
+            if (t.joinable()) t.join();
+        comp_.clear();
         std::lock_guard<std::mutex> lk(m_);
         for (auto& s : slots_) b_.release(s);
         prepared_ = false;
@@ -230,14 +247,20 @@ class CoalescingQueue {
         if (!prepared_ || stop_) return kQueueStopped;
         const uint64_t need = r.kind == QReq::kChunks ? qalign(r.len, 64) : qalign(r.len, 16);
         if (r.len > max_req_) return kQueueTooBig;  // callers check accepts() first
+        active_++;
         QSlot* s = nullptr;
         for (;;) {
             if (open_ >= 0) {
                 QSlot& o = slots_[open_];
-                if (o.nreq() < c_.max_reqs && o.lo + need <= o.hi) {
+                if (o.nreq() < c_.max_reqs && o.lo + need <= o.hi && b_.admits(o, r)) {
                     s = &o;
                     break;
                 }
+                if (o.nreq() == 0) {  // not even an empty slot takes it
+                    active_--;
+                    return kQueueTooBig;
+                }
+                o.full = true;  // launch it without lingering
             }
             if (open_ < 0) {  // open a free slot
                 for (size_t i = 0; i < slots_.size(); i++)
@@ -252,17 +275,22 @@ class CoalescingQueue {
                         f.max_chunk_len = 0;
                         f.copying = f.readers = 0;
                         f.status = 0;
+                        f.full = false;
                         f.seq = ++seq_;
+                        f.t_open = std::chrono::steady_clock::now();
                         open_ = (int)i;
                         break;
                     }
                 if (open_ >= 0) continue;
             }
-            // the open slot is full (the dispatcher launches it as soon as it may) or every slot
-            // is busy: wait for space
+            // the open slot is full (the dispatcher launches it as soon as a lane is idle) or
+            // every slot is busy: wait for space
             cv_disp_.notify_one();
             cv_space_.wait(lk);
-            if (stop_) return kQueueStopped;
+            if (stop_) {
+                active_--;
+                return kQueueStopped;
+            }
         }
         r.slot = open_;
         r.done = false;
@@ -283,16 +311,18 @@ class CoalescingQueue {
             r.idx = (uint32_t)s->hashes.size();
             s->hashes.push_back(&r);
         }
+        if (s->nreq() >= c_.max_reqs || s->hi - s->lo < max_req_) s->full = true;
         s->copying++;
         cv_disp_.notify_one();
         lk.unlock();
         if (r.len) memcpy(s->in + r.off, r.src, r.len);
         lk.lock();
         if (--s->copying == 0) cv_disp_.notify_all();
-        cv_done_.wait(lk, [&] { return r.done; });
+        done_cv_[r.slot].wait(lk, [&] { return r.done; });  // woken with its own slot only
         lk.unlock();
         const int rc = read(*s, r, r.status);
         lk.lock();
+        active_--;
         if (--s->readers == 0) {
             s->state = QSlot::kFree;
             cv_space_.notify_all();
@@ -309,48 +339,93 @@ class CoalescingQueue {
         std::lock_guard<std::mutex> lk(m_);
         return served_;
     }
+    // mean microseconds per completed batch: open -> closed (filling), closed -> launched (the
+    // callers' copies), launched -> completion observed (transfers + kernels)
+    void timing(double* fill_us, double* copy_us, double* device_us) {
+        std::lock_guard<std::mutex> lk(m_);
+        const double n = timed_ ? (double)timed_ : 1.0;
+        if (fill_us) *fill_us = t_fill_ / n;
+        if (copy_us) *copy_us = t_copy_ / n;
+        if (device_us) *device_us = t_dev_ / n;
+    }
 
   private:
+    // Whether the open slot should go now (queue lock held); else *deadline = when it will.
+    bool ready(std::chrono::steady_clock::time_point* deadline) {
+        if (open_ < 0 || inflight_ >= c_.lanes) return false;
+        const QSlot& o = slots_[open_];
+        const size_t n = o.nreq();
+        if (n == 0) return false;
+        const size_t share = (size_t)((active_ + c_.lanes - 1) / c_.lanes);
+        if (inflight_ == 0 || o.full || n >= share) return true;
+        *deadline = o.t_open + std::chrono::microseconds(c_.linger_us);
+        return std::chrono::steady_clock::now() >= *deadline;
+    }
+
     void dispatcher() {
         std::unique_lock<std::mutex> lk(m_);
         for (;;) {
-            cv_disp_.wait(lk, [&] {
-                return stop_ || (open_ >= 0 && slots_[open_].nreq() > 0 && inflight_ < c_.max_inflight);
-            });
+            std::chrono::steady_clock::time_point deadline{};
+            while (!stop_ && !ready(&deadline)) {
+                if (deadline != std::chrono::steady_clock::time_point{}) {
+                    // a timed wait on the system clock (pthread_cond_timedwait): the steady-clock
+                    // form (pthread_cond_clockwait) is invisible to the GCC 11 ThreadSanitizer;
+                    // the deadline itself is re-checked on the steady clock above
+                    const auto left = deadline - std::chrono::steady_clock::now();
+                    cv_disp_.wait_until(lk, std::chrono::system_clock::now() +
+                                                std::chrono::duration_cast<std::chrono::system_clock::duration>(left));
+                } else {
+                    cv_disp_.wait(lk);
+                }
+                deadline = {};
+            }
             if (stop_) break;
             QSlot& s = slots_[open_];
             s.state = QSlot::kClosed;
+            s.t_close = std::chrono::steady_clock::now();
             open_ = -1;
             inflight_++;
+            int lane = 0;  // an idle lane exists: inflight_ <= lanes
+            for (int l = 1; l < c_.lanes; l++)
+                if (lane_busy_[l] < lane_busy_[lane]) lane = l;
+            lane_busy_[lane]++;
             cv_space_.notify_all();  // waiting callers may open the next slot now
             cv_disp_.wait(lk, [&] { return s.copying == 0; });
             s.readers = (int)s.nreq();
             launched_++;
             served_ += s.nreq();
+            s.t_launch = std::chrono::steady_clock::now();
             lk.unlock();
-            const int rc = b_.launch(s);
+            const int rc = b_.launch(s, lane);
             lk.lock();
             s.status = rc;
             s.state = QSlot::kFlight;
-            flight_.push_back(&s);
-            cv_comp_.notify_one();
+            flight_[lane].push_back(&s);
+            comp_cv_[lane].notify_one();
         }
     }
 
-    void completer() {
+    // One per lane: a lane's batches complete in launch order (one stream).
+    void completer(int lane) {
         std::unique_lock<std::mutex> lk(m_);
         for (;;) {
-            cv_comp_.wait(lk, [&] { return !flight_.empty() || (stop_ && inflight_ == 0); });
-            if (flight_.empty()) break;  // stop_ and nothing in flight
-            QSlot* s = flight_.front();
-            flight_.pop_front();
+            comp_cv_[lane].wait(lk, [&] { return !flight_[lane].empty() || (stop_ && inflight_ == 0); });
+            if (flight_[lane].empty()) break;  // stop_ and nothing in flight
+            QSlot* s = flight_[lane].front();
+            flight_[lane].pop_front();
             const int launched_rc = s->status;
             lk.unlock();
             const int rc = b_.wait(*s);  // always: drains whatever a failed launch enqueued
             lk.lock();
             s->status = launched_rc ? launched_rc : rc;
             s->state = QSlot::kDone;
+            s->t_done = std::chrono::steady_clock::now();
+            t_fill_ += std::chrono::duration<double, std::micro>(s->t_close - s->t_open).count();
+            t_copy_ += std::chrono::duration<double, std::micro>(s->t_launch - s->t_close).count();
+            t_dev_ += std::chrono::duration<double, std::micro>(s->t_done - s->t_launch).count();
+            timed_++;
             inflight_--;
+            lane_busy_[lane]--;
             for (QReq* q : s->chunks) {
                 q->status = s->status;
                 q->done = true;
@@ -359,8 +434,10 @@ class CoalescingQueue {
                 q->status = s->status;
                 q->done = true;
             }
-            cv_done_.notify_all();
+            done_cv_[s - slots_.data()].notify_all();
             cv_disp_.notify_all();
+            if (stop_ && inflight_ == 0)
+                for (auto& cv : comp_cv_) cv.notify_all();
         }
     }
 
@@ -368,16 +445,22 @@ class CoalescingQueue {
     Config c_;
     std::vector<QSlot> slots_;
     std::mutex m_;
-    std::condition_variable cv_disp_, cv_comp_, cv_done_, cv_space_;
-    std::deque<QSlot*> flight_;
-    std::thread disp_, comp_;
+    std::condition_variable cv_disp_, cv_space_;
+    std::vector<std::condition_variable> done_cv_;  // per slot: its callers wait for its batch
+    std::vector<std::deque<QSlot*>> flight_;        // per lane, in launch order
+    std::vector<std::condition_variable> comp_cv_;  // per lane
+    std::vector<int> lane_busy_;
+    std::thread disp_;
+    std::vector<std::thread> comp_;
     int open_ = -1;
     int inflight_ = 0;
+    int active_ = 0;  // callers inside run()
     bool prepared_ = false;
     bool stop_ = false;
     uint64_t max_req_ = 0;
     uint64_t seq_ = 0;
-    uint64_t launched_ = 0, served_ = 0;
+    uint64_t launched_ = 0, served_ = 0, timed_ = 0;
+    double t_fill_ = 0, t_copy_ = 0, t_dev_ = 0;
 };
 
 }  // namespace sdfs

@@ -279,6 +279,12 @@ class HipVariableSha256HashEngine:
     def sync(self) -> None:
         check(self._lib.sdfs_cdc_stream_sync(self._h))
 
+    def queue_timing(self) -> dict:
+        """Mean microseconds per coalesced GPU pass: filling, callers' copies, device."""
+        f, c, d = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(self._lib.sdfs_cdc_queue_timing(self._h, ctypes.byref(f), ctypes.byref(c), ctypes.byref(d)))
+        return {"fill_us": round(f.value, 1), "copy_us": round(c.value, 1), "device_us": round(d.value, 1)}
+
     def queue_stats(self) -> tuple[int, int]:
         """(GPU passes launched, getChunks/getHash calls served) by the coalescing queue."""
         b, r = ctypes.c_uint64(), ctypes.c_uint64()

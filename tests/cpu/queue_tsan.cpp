@@ -48,7 +48,12 @@ struct CpuBackend {
         delete static_cast<CpuSlot*>(s.dev);
         s.dev = nullptr;
     }
-    int launch(QSlot& s) {
+    bool admits(const QSlot& s, const QReq& r) {
+        (void)r;
+        return s.chunks.size() < 200;  // a result-image limit below max_reqs (exercises the hook)
+    }
+    int launch(QSlot& s, int lane) {
+        (void)lane;
         launches++;
         auto* d = static_cast<CpuSlot*>(s.dev);
         int f = fail_batches.load();
@@ -83,9 +88,10 @@ static int stress(int nthreads, int per_thread, uint64_t slot_bytes, int fail_ba
     CpuBackend b;
     b.slot_bytes = slot_bytes;
     CoalescingQueue<CpuBackend>::Config c;
-    c.nslots = 4;
-    c.max_inflight = 2;
+    c.nslots = 5;
+    c.lanes = 3;
     c.max_reqs = 256;
+    c.linger_us = 100;
     CoalescingQueue<CpuBackend> q(b, c);
     if (q.start() != 0) return 1;
     b.fail_batches = fail_batches;
