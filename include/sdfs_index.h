@@ -68,6 +68,10 @@ int sdfs_cdc_index_clear(sdfs_cdc_index* ix, void* stream);
  * (AbstractHashesMap.getSize / getMaxSize) */
 int sdfs_cdc_index_size(sdfs_cdc_index* ix, uint64_t* used, uint64_t* capacity);
 
+/* Test hook: the batch epoch counter (31 bits; the next put_records uses epoch + 1, wrapping to 1).
+ * Stamps only mark a batch's own insertions while it runs, so any value is safe. */
+int sdfs_cdc_index_set_epoch(sdfs_cdc_index* ix, uint32_t epoch);
+
 #ifdef __cplusplus
 }
 #endif

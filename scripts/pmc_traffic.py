@@ -52,11 +52,15 @@ def main():
     ap.add_argument("-o", "--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                          "pmc_traffic.json"))
     ap.add_argument("--skip", type=int, default=1, help="launches to drop per kernel (warmup)")
+    ap.add_argument("--params", default="", help="the bench's config.params string these passes measured")
+    ap.add_argument("--source", default="", help="what was profiled (command / profile directory)")
+    ap.add_argument("--commit", default="", help="git commit of the measured code")
     a = ap.parse_args()
     fetch = read_counter(a.fetch_dir, "FETCH_SIZE")
     write = read_counter(a.write_dir, "WRITE_SIZE")
     out = {"_note": "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024, mean over launches "
-                    "after warmup; FETCH_SIZE/WRITE_SIZE in KiB (rocprofv3, gfx950 x2 read correction)"}
+                    "after warmup; FETCH_SIZE/WRITE_SIZE in KiB (rocprofv3, gfx950 x2 read correction)",
+           "params": a.params, "source": a.source, "commit": a.commit}
     for stage in sorted(set(fetch) | set(write)):
         f = fetch.get(stage, [])[a.skip:] or fetch.get(stage, [])
         w = write.get(stage, [])[a.skip:] or write.get(stage, [])

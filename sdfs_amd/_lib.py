@@ -111,6 +111,7 @@ SIGNATURES = {
     "sdfs_cdc_index_get": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
     "sdfs_cdc_index_size": (ctypes.c_int, [_vp, _u64p, _u64p]),
     "sdfs_cdc_index_clear": (ctypes.c_int, [_vp, _vp]),
+    "sdfs_cdc_index_set_epoch": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     # include/sdfs_lz4.h
     "sdfs_cdc_lz4_bound": (ctypes.c_uint64, [ctypes.c_uint64]),
     "sdfs_cdc_lz4_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P(_vp)]),

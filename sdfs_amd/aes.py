@@ -12,8 +12,11 @@ and the archive's 16-byte IV — and read back with ``decryptCBC`` (HashBlobArch
   on the fly.
 * :func:`key_from_passphrase` — EncryptUtils' key derivation (host control logic, once).
 
-No CPU fallback: every call runs the HIP kernels and raises :class:`SdfsCdcError` on failure;
-``decryptCBC`` raises ``IOError`` on bad padding as ``EncryptUtils.decryptCBC`` does.
+No CPU fallback: every call runs the HIP kernels and raises :class:`SdfsCdcError` on failure.
+``decryptCBC`` retries a record whose padding is bad under the legacy key SHA-256("Password") and
+raises ``IOError`` only if that fails too, as ``EncryptUtils.decryptCBC`` does
+(EncryptUtils.java:50-52,131-149); the device form does the same for the records that fail when
+``legacy_fallback`` is set (a second GPU pass over just those records).
 """
 from __future__ import annotations
 
@@ -26,6 +29,9 @@ from . import _lib
 from ._lib import check
 
 BAD_PADDING = 0xFFFFFFFF
+# EncryptUtils.oldKeyBytes = getSHAHashBytes("Password".getBytes()) (EncryptUtils.java:50): the key of
+# chunk stores written before the passphrase became configurable; decryptCBC falls back to it
+LEGACY_KEY = hashlib.sha256(b"Password").digest()
 
 
 def key_from_passphrase(passphrase: str) -> bytes:
@@ -56,12 +62,24 @@ class HipEncryptUtils:
         check(self._lib.sdfs_cdc_aes_create(int(device), k.ctypes.data, len(k), ctypes.byref(h)))
         self._h = h
         self.device = device
+        self._key = bytes(k)
+        self._legacy = None  # engine under LEGACY_KEY, created on the first record that needs it
+
+    def _legacy_engine(self) -> "HipEncryptUtils | None":
+        if self._key == LEGACY_KEY:
+            return None
+        if self._legacy is None:
+            self._legacy = HipEncryptUtils(LEGACY_KEY, self.device)
+        return self._legacy
 
     @classmethod
     def from_passphrase(cls, passphrase: str, device: int = 0) -> "HipEncryptUtils":
         return cls(key_from_passphrase(passphrase), device)
 
     def destroy(self) -> None:
+        if getattr(self, "_legacy", None) is not None:
+            self._legacy.destroy()
+            self._legacy = None
         if getattr(self, "_h", None):
             self._lib.sdfs_cdc_aes_destroy(self._h)
             self._h = None
@@ -93,17 +111,29 @@ class HipEncryptUtils:
                                              ctypes.byref(n)))
         return out[: n.value].tobytes()
 
-    def decryptCBC(self, enc, iv) -> bytes:
-        """EncryptUtils.decryptCBC(encChunk, ivspec); IOError on a bad length or padding."""
-        a, v = _u8(enc), self._iv(iv)
-        if len(a) == 0 or len(a) % 16:
-            raise IOError("ciphertext length is not a positive multiple of 16")
+    def _decrypt_one(self, a: np.ndarray, v: np.ndarray) -> int | bytes:
         out = np.zeros(len(a), np.uint8)
         n = ctypes.c_uint64()
         rc = self._lib.sdfs_cdc_aes_decrypt(self._h, a.ctypes.data, len(a), v.ctypes.data, out.ctypes.data,
                                             len(a), ctypes.byref(n))
-        check(rc)  # SdfsCdcError is an IOError (bad padding -> EINVAL)
-        return out[: n.value].tobytes()
+        return out[: n.value].tobytes() if rc == _lib.OK else rc
+
+    def decryptCBC(self, enc, iv) -> bytes:
+        """EncryptUtils.decryptCBC(encChunk, ivspec) (EncryptUtils.java:131-149): bad padding under
+        the configured key -> retry under the legacy key; IOError if both fail."""
+        a, v = _u8(enc), self._iv(iv)
+        if len(a) == 0 or len(a) % 16:
+            raise IOError("ciphertext length is not a positive multiple of 16")
+        r = self._decrypt_one(a, v)
+        if isinstance(r, bytes):
+            return r
+        legacy = self._legacy_engine() if r == _lib.EINVAL else None  # EINVAL = bad padding
+        if legacy is not None:
+            r2 = legacy._decrypt_one(a, v)
+            if isinstance(r2, bytes):
+                return r2
+        check(r)  # SdfsCdcError is an IOError
+        raise IOError("decryption failed")
 
     # ---- batches
     def encrypt_chunks(self, base, offs, lens, iv, nz_prefix: int | None = None) -> list[bytes]:
@@ -144,8 +174,11 @@ class HipEncryptUtils:
             dst_off.data_ptr(), dst_len.data_ptr(), s))
 
     def decrypt_device(self, data, src_off, src_len, out, dst_off, dst_len, iv=None, ivs=None, count=None,
-                       stream=None) -> None:
-        """Inverse of encrypt_device; dst_len[i] = plaintext length or 0xFFFFFFFF (bad padding)."""
+                       stream=None, legacy_fallback: bool = False) -> None:
+        """Inverse of encrypt_device; dst_len[i] = plaintext length or 0xFFFFFFFF (bad padding).
+        legacy_fallback: records with bad padding are decrypted again under the legacy key
+        (EncryptUtils.decryptCBC's retry) in a second pass over just those records; this waits
+        for the first pass on the host to find them."""
         import torch
 
         n = int(src_len.shape[0])
@@ -155,3 +188,21 @@ class HipEncryptUtils:
             self._h, data.data_ptr(), src_off.data_ptr(), src_len.data_ptr(),
             count.data_ptr() if count is not None else None, n, v.ctypes.data if v is not None else None,
             ivs.data_ptr() if ivs is not None else None, out.data_ptr(), dst_off.data_ptr(), dst_len.data_ptr(), s))
+        legacy = self._legacy_engine() if legacy_fallback else None
+        if legacy is None or n == 0:
+            return
+        st = torch.cuda.ExternalStream(s, device=data.device) if not isinstance(s, torch.cuda.Stream) else s
+        with torch.cuda.stream(st):
+            live = torch.arange(n, device=dst_len.device)
+            if count is not None:
+                live = live[live < count.to(torch.int64).reshape(())]
+            bad = live[dst_len.view(torch.int32)[live] == -1]  # 0xFFFFFFFF
+            k = int(bad.numel())  # host sync: the retry needs the failed records' count
+            if k == 0:
+                return
+            sub_off, sub_len, sub_dst = src_off[bad].contiguous(), src_len[bad].contiguous(), dst_off[bad].contiguous()
+            sub_ivs = ivs[bad].contiguous() if ivs is not None else None
+            sub_out_len = torch.empty_like(sub_len)
+            legacy.decrypt_device(data, sub_off, sub_len, out, sub_dst, sub_out_len, iv=iv, ivs=sub_ivs,
+                                  stream=st.cuda_stream)
+            dst_len[bad] = sub_out_len.to(dst_len.dtype)

@@ -17,7 +17,9 @@
 //   2. probe   — one lane per group representative probes the global table: hit -> refcount +=
 //                claims; miss -> claim an empty slot with a CAS on its state word, stamped with
 //                this batch's epoch (lanes of the same batch skip each other's fresh slots without
-//                reading their keys: representatives are distinct fingerprints);
+//                reading their keys: representatives are distinct fingerprints); the assign step
+//                turns every stamp of the batch into the committed state, so no stamp outlives
+//                its batch (epochs may wrap);
 //   3-4. rank  — block counts + one-block scan of the "inserted" flags in record order;
 //   5. assign  — inserted record -> new_list[rank], slot pos = pos_base + rank;
 //   6. output  — per record: dup = not inserted, hashloc = its fingerprint's pos.
@@ -39,12 +41,14 @@ struct alignas(64) IndexSlot {
     uint4 key[2];     // digest, zero-padded to 32 bytes
     uint64_t pos;     // where the chunk lives (caller's namespace)
     uint64_t ref;     // reference count
-    uint32_t state;   // 0 = empty, else (epoch << 1) | 1
+    uint32_t state;   // 0 = empty, kCommitted = holds a fingerprint, (epoch << 1) | 1 (epoch >= 1) =
+                      // being inserted by the batch of that epoch
     uint32_t pad[3];
 };
 static_assert(sizeof(IndexSlot) == 64, "one cache line per slot");
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kCommitted = 1u;  // never a batch stamp: those are >= 3
 constexpr int kIxThreads = 256;
 constexpr int kRankBlock = 1024;
 
@@ -217,7 +221,9 @@ __global__ __launch_bounds__(kRankBlock) void ix_assign_kernel(const uint32_t* d
     if (f) {
         const uint32_t rank = bbase[blockIdx.x] + ex;
         if (new_list) new_list[rank] = r;
-        table[gidx[lslot[r]]].pos = pos_base + rank;
+        IndexSlot& slot = table[gidx[lslot[r]]];
+        slot.pos = pos_base + rank;
+        slot.state = kCommitted;  // the batch stamp must not survive the batch
     }
 }
 
@@ -437,6 +443,13 @@ int sdfs_cdc_index_clear(sdfs_cdc_index* ix, void* stream) {
     IX_TRY(hipMemsetAsync(ix->overflow.p, 0, sizeof(uint32_t), s));
     ix->used_ub = 0;
     ix->last = s;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_index_set_epoch(sdfs_cdc_index* ix, uint32_t epoch) {
+    if (!ix) return fail_status(SDFS_CDC_EINVAL, "null index");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    ix->epoch = epoch & 0x7FFFFFFFu;  // the next batch uses epoch + 1 (wrapping to 1)
     return SDFS_CDC_OK;
 }
 

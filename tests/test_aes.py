@@ -239,6 +239,61 @@ def test_gpu_device_path_ivs_count_and_decrypt():
         assert b[src_off[i]: src_off[i] + lens[i]].tobytes() == data[src_off[i]: src_off[i] + lens[i]].tobytes(), i
 
 
+def _oracle_decrypt_with_fallback(key, iv, ct):
+    """EncryptUtils.decryptCBC (EncryptUtils.java:131-149): the configured key, then the legacy key."""
+    from sdfs_amd.aes import LEGACY_KEY
+    for k in (key, LEGACY_KEY):
+        try:
+            return A.cbc_decrypt(k, iv, ct)
+        except ValueError:
+            continue
+    return None
+
+
+@pytest.mark.gpu
+def test_gpu_decrypt_legacy_key_fallback():
+    """Records written under the legacy key SHA-256("Password") (EncryptUtils.java:50) decrypt
+    through the fallback, on the host form and in the device form's second pass."""
+    import torch
+
+    from sdfs_amd.aes import LEGACY_KEY
+
+    key = _key(32, 4)
+    c, old = ciph(key), ciph(LEGACY_KEY)
+    iv = bytes(range(7, 23))
+    datas = [C.synth(9, i, 0, n).tobytes() for i, n in enumerate([0, 1, 15, 16, 100, 4096, 33000, 777] * 6)]
+    cts = [(old if i % 3 == 0 else c).encryptCBC(d, iv) for i, d in enumerate(datas)]
+    for i, (d, ct) in enumerate(zip(datas, cts)):
+        assert c.decryptCBC(ct, iv) == d, i
+    bad = bytearray(cts[4])
+    bad[-1] ^= 0x33
+    want_bad = _oracle_decrypt_with_fallback(key, iv, bytes(bad))
+    if want_bad is None:
+        with pytest.raises(IOError):
+            c.decryptCBC(bytes(bad), iv)
+    cts[4] = bytes(bad)
+    # device form: all records in one buffer, fallback pass for the legacy ones
+    dev = torch.device("cuda:0")
+    src_off = np.concatenate([[0], np.cumsum([len(x) + 16 for x in cts[:-1]])]).astype(np.int64)
+    buf = np.zeros(int(src_off[-1]) + len(cts[-1]) + 16, np.uint8)
+    for o, x in zip(src_off, cts):
+        buf[int(o): int(o) + len(x)] = np.frombuffer(x, np.uint8)
+    dst_off = src_off.copy()
+    out = torch.zeros(len(buf), dtype=torch.uint8, device=dev)
+    plen = torch.zeros(len(cts), dtype=torch.int32, device=dev)
+    c.decrypt_device(torch.from_numpy(buf).to(dev), torch.from_numpy(src_off).to(dev),
+                     torch.tensor([len(x) for x in cts], dtype=torch.int32, device=dev), out,
+                     torch.from_numpy(dst_off).to(dev), plen, iv=iv, legacy_fallback=True)
+    torch.cuda.synchronize()
+    o, pl = out.cpu().numpy(), plen.cpu().numpy().view(np.uint32)
+    for i, ct in enumerate(cts):
+        want = _oracle_decrypt_with_fallback(key, iv, ct)
+        if want is None:
+            assert pl[i] == 0xFFFFFFFF, i
+        else:
+            assert pl[i] == len(want) and o[dst_off[i]: dst_off[i] + pl[i]].tobytes() == want, i
+
+
 @pytest.mark.gpu
 def test_gpu_lz4_then_aes_chain():
     """Compressed + encrypted chunk store: AES of the framed LZ4 record, all on the device."""

@@ -163,6 +163,32 @@ def test_index_device_count_and_empty_batch():
 
 
 @pytest.mark.gpu
+def test_index_epoch_wrap_keeps_dedup():
+    """A batch's insertion stamp must not outlive the batch: with the epoch counter wrapped so that
+    a later batch reuses an earlier batch's stamp, re-putting the same fingerprints finds every
+    one of them (a surviving stamp made the probe skip the slot and insert twice)."""
+    torch = pytest.importorskip("torch")
+    from sdfs_amd.index import HipHashesMap
+    rng = random.Random(17)
+    ix = HipHashesMap(4096)
+    lib = _lib.load()
+    digests = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(300)]
+    rec = _records(digests, list(range(300)))
+    _lib.check(lib.sdfs_cdc_index_set_epoch(ix._h, 0x7FFFFFFE))  # next batch: the last epoch
+    dup, loc, new = _put(ix, torch, rec, 1000)
+    assert sum(dup) == 0 and len(new) == 300
+    _lib.check(lib.sdfs_cdc_index_set_epoch(ix._h, 0x7FFFFFFE))  # the same stamp again
+    dup2, loc2, new2 = _put(ix, torch, rec, 5000)
+    assert all(d == 1 for d in dup2) and new2 == [] and loc2 == loc
+    dup3, _, new3 = _put(ix, torch, rec, 9000)  # epoch wraps to 1 here
+    assert all(d == 1 for d in dup3) and new3 == []
+    assert ix.getSize() == 300
+    pos, ref = ix.get_digests(ix._digest_tensor(digests[:10]))
+    assert ref.cpu().tolist() == [3] * 10
+    ix.destroy()
+
+
+@pytest.mark.gpu
 def test_index_full_raises():
     torch = pytest.importorskip("torch")
     from sdfs_amd.index import HipHashesMap
