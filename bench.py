@@ -27,9 +27,16 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz int32 ops/s
-# VALU instructions per input byte, counted in the production ISA: scan 10 per byte
-# (+ block overhead), SHA-256 1383 per 64-byte block + one padding block per chunk
-OPS_PER_BYTE = {"cdc_scan": 10.2, "chunk_hash": 21.9}
+# VALU instructions per input byte per lane (SQ_INSTS_VALU / (bytes / 64), rocprofv3 PMC of the
+# production kernels, profiles/r02/start/pmc_summary.json): scan 10.8, SHA-256 22.4 (1423 per
+# 64-byte block incl. one padding block per chunk)
+OPS_PER_BYTE = {"cdc_scan": 10.8, "chunk_hash": 22.4}
+# SIMD issue cycles per wave-byte: the ISA mix of each kernel's loop weighted by the measured issue
+# cost of each instruction (scripts/isa_microbench.hip, profiles/r01/isa_microbench.txt: 2.0 for
+# xor/and/shift, 2.2 bitop3, 2.4 add/addc, 3.6 alignbit/perm/add3); the clock the microbenchmark
+# calibrates to under full VALU load is 2.07 GHz.  valu_busy = issue cycles / (SIMDs x clock x time).
+VALU_CYCLES_PER_BYTE = {"cdc_scan": 26.0, "chunk_hash": 4180.0 / 64 * 1.008}
+SIMDS, VALU_CLOCK_HZ = 256 * 4, 2.07e9
 METRIC = "device-resident GiB/s CDC+fingerprint, 4 KiB-mean chunks, 1/2/4/8 MI355X"
 
 
@@ -114,9 +121,13 @@ class TwoStreamRunner:
         i = self.k & 1
         self.k += 1
         b, s = self.batches[i], self.streams[i]
+        rec = None
+        if exchange is not None and exchange.direct:
+            rec = exchange.acquire(stream=s)  # the engine writes its records into the exchange slot
+            b.set_records(rec)
         b.run(buffer_id_base=buffer_id_base, stream=s.cuda_stream)
         if exchange is not None:
-            exchange.submit(b.recs.view(-1, 48), b.total, stream=s)
+            exchange.submit(rec if rec is not None else b.recs.view(-1, 48), b.total, stream=s)
 
     def identical(self) -> bool:
         t = self.torch
@@ -194,6 +205,8 @@ def main():
     ap.add_argument("--compare", type=int, default=1, help="also time the other streams-in-flight mode (N = 1)")
     ap.add_argument("--exchange", type=int, default=-1,
                     help="record all-gather: -1 = when N > 1, 1 = also at N = 1 (exercises the path)")
+    ap.add_argument("--exchange-mode", default="direct", choices=["direct", "copy"],
+                    help="direct: the engine writes records into the exchange slot; copy: snapshot copy")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -234,15 +247,24 @@ def main():
     nsf = args.streams_in_flight
     # N > 1: the one real exchange (all-gather of the fingerprint records), pipelined on a side
     # stream so step i's table travels while step i+1 is chunked (sdfs_amd/dist.py)
-    ex = RecordExchange(batch.recs.view(-1, 48).shape[0], device) if use_ex else None
+    ex = None
+    if use_ex:
+        direct = args.exchange_mode == "direct"
+        # direct: a third slot, so a step's slot was all-gathered a step before it is rewritten
+        ex = RecordExchange(batch.recs.view(-1, 48).shape[0], device, depth=2, slots=3 if direct else 2)
+        ex.direct = direct
 
     def step():
         if nsf == 2:
             runner.step(base_id, ex)
         else:
+            rec = None
+            if ex is not None and ex.direct:
+                rec = ex.acquire(stream=cs)
+                batch.set_records(rec)
             batch.run(buffer_id_base=base_id, stream=cs.cuda_stream)
             if ex is not None:
-                ex.submit(batch.recs.view(-1, 48), batch.total, stream=cs)
+                ex.submit(rec if rec is not None else batch.recs.view(-1, 48), batch.total, stream=cs)
 
     def drain():
         if ex is not None:
@@ -365,6 +387,8 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     valu = {k: round(nbytes * OPS_PER_BYTE[k] / (kt_one[k] / 1e3) / VALU_PEAK_OPS, 3) for k in OPS_PER_BYTE
             if kt_one.get(k)}
+    valu_busy = {k: round(nbytes / 64 * VALU_CYCLES_PER_BYTE[k] / (SIMDS * VALU_CLOCK_HZ * kt_one[k] / 1e3), 3)
+                 for k in VALU_CYCLES_PER_BYTE if kt_one.get(k)}
     params = (f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
               f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen {args.hash_type}")
     traffic, traffic_src = load_traffic("chunk_hash", params)
@@ -404,7 +428,8 @@ def main():
             "chunks_per_gpu_step": total,
             "streams_in_flight": nsf,
             "records_identical_across_streams": identical,
-            "exchange": "RCCL all_gather of 48-B fingerprint records, pipelined" if use_ex else "none (N=1)",
+            "exchange": (f"RCCL all_gather of 48-B fingerprint records, pipelined ({args.exchange_mode})"
+                         if use_ex else "none (N=1)"),
             "parallelism": f"dp{world} (streams sharded per GPU)",
         },
         "kernels_ms": {k: round(v, 4) for k, v in kt.items()},
@@ -423,6 +448,7 @@ def main():
             "achieved_per_step": round(nbytes / (ms_step / 1e3) / 1e9, 1),
             "frac_per_step": round(nbytes / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
             "valu_frac": valu,
+            "valu_busy": valu_busy,
         },
         "cpu_baseline": cpu,
         "one_stream" if nsf == 2 else "two_streams": other,

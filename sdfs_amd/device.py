@@ -51,6 +51,19 @@ class DeviceBatch:
             records=self.recs.data_ptr() if self.recs is not None else None,
             records_cap=nslots if self.recs is not None else 0, total=self.total.data_ptr())
 
+    def set_records(self, table) -> None:
+        """Have the engine write the fingerprint records straight into ``table`` (a [>= nbuf*cap,
+        48] uint8 device tensor, e.g. a :class:`sdfs_amd.dist.RecordExchange` slot) instead of this
+        batch's own record buffer: the exchange then all-gathers them with no snapshot copy."""
+        rows = table.shape[0] if table.dim() == 2 else table.numel() // _lib.RECORD_BYTES
+        if table.device != self.data.device or not table.is_contiguous():
+            raise ValueError("record table must be a contiguous tensor on the batch's device")
+        if rows < self.nbuf * self.cap:
+            raise ValueError(f"record table holds {rows} records, the batch may write {self.nbuf * self.cap}")
+        self.recs = table.view(-1)
+        self.out.records = table.data_ptr()
+        self.out.records_cap = rows
+
     @property
     def nbytes(self) -> int:
         return self.nbuf * self.buf_len

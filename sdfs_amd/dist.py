@@ -56,67 +56,113 @@ def allgather_records(table: torch.Tensor, count: int | torch.Tensor, group=None
 class RecordExchange:
     """Pipelined all-gather of per-step fingerprint tables.
 
-    ``submit(table, count)`` snapshots ``table[:capacity]`` and the device ``count`` on the
-    producer stream (no host sync) and starts the count all-gather on a side stream; the table
-    all-gather of a step is issued when the pipeline is ``depth`` steps deep (or on ``flush``),
-    after its counts are known on the side stream.  The producer stream only waits for a slot's
-    previous exchange before overwriting it.  Results are ``(gathered, counts)``: gathered is
-    [world * max(counts), 48] in rank order, rank r's rows at [r * max, r * max + counts[r]).
-    On CPU tensors (gloo) every call is synchronous.
+    ``submit(table, count)`` hands over step i's table and its device ``count`` on the producer
+    stream (no host sync) and starts the count all-gather on a side stream; the table all-gather
+    of a step is issued when ``depth`` steps are pending (or on ``flush``), after its counts are
+    known on the side stream.  Tables live in a ring of ``slots`` buffers (default ``depth``).
+    Two ways to fill a slot:
+
+    * copy: ``submit`` snapshots ``table[:capacity]`` into the slot on the producer stream;
+    * direct: ``acquire()`` returns the next slot for the engine to write its records into
+      (``DeviceBatch.set_records``); ``submit`` of that same tensor copies nothing.  With
+      ``slots > depth`` the slot's previous all-gather was issued a step earlier, so acquiring it
+      never waits on the host — the producer stream only waits for that all-gather's event.
+
+    Results are ``(gathered, counts)``: gathered is [world * max(counts), 48] in rank order, rank
+    r's rows at [r * max, r * max + counts[r]).  On CPU tensors (gloo) every call is synchronous.
     """
 
-    def __init__(self, capacity: int, device, group=None, depth: int = 2):
+    def __init__(self, capacity: int, device, group=None, depth: int = 2, slots: int | None = None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.capacity = int(capacity)
         self.depth = max(1, int(depth))
+        self.nslots = max(self.depth, int(slots or self.depth))
         self.slots = [torch.empty(self.capacity, RECORD_BYTES, dtype=torch.uint8, device=self.device)
-                      for _ in range(self.depth)]
-        self.cnt = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.depth)]
-        self.counts = [torch.zeros(self.world, dtype=torch.int64, device=self.device) for _ in range(self.depth)]
-        self.free = [None] * self.depth  # side-stream event after a slot's table all-gather
+                      for _ in range(self.nslots)]
+        self.cnt = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.nslots)]
+        self.counts = [torch.zeros(self.world, dtype=torch.int64, device=self.device) for _ in range(self.nslots)]
+        self.free = [None] * self.nslots  # side-stream event after a slot's table all-gather
+        # counts reach the host through pinned memory + an event of their own: reading them must
+        # not synchronise the whole side stream (that would wait for the newest step's production)
+        self.counts_host = [torch.zeros(self.world, dtype=torch.int64, pin_memory=self.cuda)
+                            for _ in range(self.nslots)]
+        self.counts_ev = [None] * self.nslots
         self.side = torch.cuda.Stream(self.device) if self.cuda else None
-        self.pending = deque()
+        self.pending = deque()  # slots submitted, table all-gather not issued yet (oldest first)
         self.results = []
         self.n = 0
+        self.direct = False  # callers that acquire() slots for the engine set this (bench.py)
 
     def _ctx(self):
         import contextlib
         return torch.cuda.stream(self.side) if self.cuda else contextlib.nullcontext()
 
-    def submit(self, table: torch.Tensor, count, stream=None) -> None:
-        if len(self.pending) == self.depth:
+    def _producer(self, stream):
+        prod = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if not isinstance(prod, torch.cuda.Stream):
+            prod = torch.cuda.ExternalStream(prod, device=self.device)
+        return prod
+
+    def _reclaim(self, slot: int, prod) -> None:
+        """Make `slot` writable for the producer: issue its pending all-gather if it still has
+        one (only when slots == depth), then order the producer after that all-gather."""
+        while slot in self.pending:
             self.results.append(self._finish(self.pending.popleft()))
-        slot = self.n % self.depth
+        if self.cuda and self.free[slot] is not None:
+            prod.wait_event(self.free[slot])
+            self.free[slot] = None
+
+    def acquire(self, stream=None) -> torch.Tensor:
+        """The slot the NEXT submit will exchange, free for the producer to write (see class doc)."""
+        slot = self.n % self.nslots
+        self._reclaim(slot, self._producer(stream) if self.cuda else None)
+        return self.slots[slot]
+
+    def submit(self, table: torch.Tensor, count, stream=None) -> None:
+        # issue the oldest pending table all-gather BEFORE this step's count all-gather: torch's
+        # process group runs its collectives in call order on one internal stream, and this step's
+        # count exchange waits for this step's production
+        while len(self.pending) >= self.depth:
+            self.results.append(self._finish(self.pending.popleft()))
+        slot = self.n % self.nslots
         self.n += 1
-        prod = None
-        if self.cuda:
-            prod = stream if stream is not None else torch.cuda.current_stream(self.device)
-            if not isinstance(prod, torch.cuda.Stream):
-                prod = torch.cuda.ExternalStream(prod, device=self.device)
-            if self.free[slot] is not None:
-                prod.wait_event(self.free[slot])
+        prod = self._producer(stream) if self.cuda else None
+        self._reclaim(slot, prod)
+        # the acquired slot itself (the engine wrote its records in place): nothing to copy
+        direct = table.data_ptr() == self.slots[slot].data_ptr()
         n = min(self.capacity, table.shape[0])
         c = count if isinstance(count, torch.Tensor) else torch.tensor([count], device=self.device)
         if self.cuda:
             with torch.cuda.stream(prod):
-                self.slots[slot][:n].copy_(table[:n], non_blocking=True)
+                if not direct:
+                    self.slots[slot][:n].copy_(table[:n], non_blocking=True)
                 self.cnt[slot].copy_(c.reshape(1).to(torch.int64), non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(prod)
             self.side.wait_event(ev)
         else:
-            self.slots[slot][:n].copy_(table[:n])
+            if not direct:
+                self.slots[slot][:n].copy_(table[:n])
             self.cnt[slot].copy_(c.reshape(1).to(torch.int64))
         with self._ctx():
             dist.all_gather_into_tensor(self.counts[slot], self.cnt[slot], group=self.group)
+            if self.cuda:
+                self.counts_host[slot].copy_(self.counts[slot], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+                self.counts_ev[slot] = ev
+            else:
+                self.counts_host[slot].copy_(self.counts[slot])
         self.pending.append(slot)
 
     def _finish(self, slot: int):
         with self._ctx():
-            cl = self.counts[slot].tolist()  # syncs the side stream only
+            if self.cuda:
+                self.counts_ev[slot].synchronize()  # this step's counts only
+            cl = self.counts_host[slot].tolist()
             if max(cl) > self.capacity:
                 raise ValueError(f"record count {max(cl)} exceeds the exchange capacity {self.capacity}")
             mx = max(cl) if cl else 0

@@ -58,23 +58,26 @@ def test_allgather_records_gloo(world):
         assert res[r] == expect
 
 
-def _exchange_worker(rank, world, port, q):
+def _exchange_worker(rank, world, port, q, direct=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cap = 12
-        ex = RecordExchange(cap, "cpu", depth=2)
+        ex = RecordExchange(cap, "cpu", depth=2, slots=3 if direct else None)
         got = []
         table = torch.zeros(cap, RECORD_BYTES, dtype=torch.uint8)
         for step in range(5):
             n = (rank * 3 + step * 2) % (cap + 1)
+            if direct:  # the producer writes into the exchange's own slot (bench.py's engine path)
+                table = ex.acquire()
             table[:] = 255  # garbage beyond the count
             for i in range(n):
                 table[i, :] = (step * 40 + rank * 10 + i) % 250
             ex.submit(table, torch.tensor([n]))
-            # the table is reused right away: the exchange must hold its own snapshot
-            table[:] = 254
+            if not direct:
+                # the table is reused right away: the exchange must hold its own snapshot
+                table[:] = 254
             if step == 2:
                 got += ex.flush()
         got += ex.flush()
@@ -83,12 +86,12 @@ def _exchange_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_record_exchange_pipelined_gloo(world):
+@pytest.mark.parametrize("world,direct", [(2, False), (3, False), (2, True), (3, True)])
+def test_record_exchange_pipelined_gloo(world, direct):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q, direct)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))

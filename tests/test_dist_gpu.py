@@ -51,6 +51,51 @@ def test_record_exchange_rccl_world1_overlapped_steps():
 
 
 @pytest.mark.gpu
+def test_record_exchange_rccl_direct_slots_two_streams():
+    """bench.py's production form: two batches in flight on two streams, each engine run writing
+    its records straight into the exchange slot it acquired (no snapshot copy)."""
+    import torch
+    import torch.distributed as dist
+
+    from sdfs_amd import HipVariableSha256HashEngine
+    from sdfs_amd.device import DeviceBatch
+    from sdfs_amd.dist import RecordExchange
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        eng = HipVariableSha256HashEngine()
+        batches = [DeviceBatch(eng, nbuf=64, buf_len=262144) for _ in range(2)]
+        ex = RecordExchange(batches[0].recs.view(-1, 48).shape[0], "cuda:0", depth=2, slots=3)
+        streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+        for k, b in enumerate(batches):  # different inputs per batch
+            b.fill_streams(first_stream=7 * k, bufs_per_stream=8)
+        torch.cuda.synchronize()
+        refs = []
+        for b in batches:  # reference records from each batch's own buffer
+            b.run()
+            torch.cuda.synchronize()
+            refs.append(b.record_table().clone())
+        for step in range(6):
+            b, s = batches[step & 1], streams[step & 1]
+            rec = ex.acquire(stream=s)
+            b.set_records(rec)
+            b.run(buffer_id_base=0, stream=s.cuda_stream)
+            ex.submit(rec, b.total, stream=s)
+        got = ex.flush()
+        torch.cuda.synchronize()
+        assert len(got) == 6
+        for step, (g, cl) in enumerate(got):
+            want = refs[step & 1]
+            assert cl == [want.shape[0]]
+            assert torch.equal(RecordExchange.compact(g, cl), want), step
+        eng.destroy()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
 def test_sharded_dedup_index_rccl_world1_matches_local_index():
     import torch
     import torch.distributed as dist
