@@ -216,6 +216,7 @@ struct sdfs_cdc_engine {
     int scan_variant = 0;     // 0 = production; others exist only in the tuning build
     int hash_variant = 0;
     int hash_wg_per_cu = 2;
+    uint32_t scan_max_block = kScanThreads;  // widest scan workgroup (tuning build: SDFS_SCAN_MAX_BLOCK)
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
@@ -447,7 +448,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     const uint64_t max_wgs = (uint64_t)e->num_cus * e->scan_info.wg_per_cu;
     const uint64_t lanes = (seg_bound + e->scan_info.chains - 1) / e->scan_info.chains;
     uint64_t block = (lanes + max_wgs - 1) / max_wgs;
-    block = std::min<uint64_t>(std::max<uint64_t>((block + 255) / 256 * 256, 256), kScanThreads);
+    block = std::min<uint64_t>(std::max<uint64_t>((block + 255) / 256 * 256, 256), e->scan_max_block);
     const uint64_t per_block = block * e->scan_info.chains;
     uint64_t grid = (seg_bound + per_block - 1) / per_block;
     grid = std::min<uint64_t>(grid, max_wgs);
@@ -1073,6 +1074,8 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     if (const char* v = getenv("SDFS_SEG_LEN")) e->seg_len = (uint32_t)atoi(v);
     if (const char* v = getenv("SDFS_HASH_VARIANT")) e->hash_variant = atoi(v);
     if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
+    if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
+        e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif
     e->scan_info = scan_variant_info(e->scan_variant);
     if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0) {
