@@ -158,7 +158,9 @@ def threads_sweep(eng_cfg, device, host, buf_len, thread_counts):
 
     out = {}
     eng = HashFunctionPool(eng_cfg, device=device).getHashEngine()
-    T.getchunks(eng, 8, host, buf_len, 64)  # warm: queue slots, pinned staging
+    # warm at the highest concurrency of the sweep, so every slot and lane has carried a pass
+    tmax = max(thread_counts) if thread_counts else 8
+    T.getchunks(eng, tmax, host, buf_len, max(256, 4 * tmax))
     start = eng.queue_stats()
     for th in thread_counts:
         calls = max(256, th * 8)

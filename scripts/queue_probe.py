@@ -24,14 +24,27 @@ torch.cuda.synchronize()
 host = b.data.cpu().numpy()
 del b
 e0.destroy()
+def cpu_stat():
+    """cgroup CPU throttling counters (cpu.stat): a quota-throttled process stalls for the rest of
+    the period, which shows up as multi-millisecond outliers in the latency tail."""
+    try:
+        return {k: int(v) for k, v in (ln.split() for ln in open("/sys/fs/cgroup/cpu.stat"))}
+    except Exception:
+        return {}
+
+
 for th in [int(x) for x in os.environ.get("THREADS", "1,32,128,384").split(",")]:
     e = HipVariableSha256HashEngine()
-    T.getchunks(e, 8, host, L, 64)
+    T.getchunks(e, th, host, L, max(256, 4 * th))  # warm: every slot and lane carries a pass
     b0 = e.queue_stats()
+    c0 = cpu_stat()
     calls = max(256, th * 8)
     r, _ = T.getchunks(e, th, host, L, calls)
+    c1 = cpu_stat()
     b1 = e.queue_stats()
+    thr = {k: c1[k] - c0.get(k, 0) for k in ("nr_throttled", "throttled_usec", "usage_usec") if k in c1}
     print(json.dumps({"threads": th, "qi": os.environ.get("SDFS_Q_INFLIGHT", "default"), "gibps": round(r.gibps, 3),
                       "p50_us": round(r.p50_us), "p99_us": round(r.p99_us), "calls_per_pass":
-                      round((b1[1] - b0[1]) / max(b1[0] - b0[0], 1), 1), **e.queue_timing()}), flush=True)
+                      round((b1[1] - b0[1]) / max(b1[0] - b0[0], 1), 1), **e.queue_timing(), "cgroup": thr}),
+          flush=True)
     e.destroy()

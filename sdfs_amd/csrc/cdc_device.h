@@ -722,6 +722,38 @@ __device__ __forceinline__ void load_block64(uint4 (&v)[4], const uint8_t* q) {
     for (int j = 0; j < 4; j++) __builtin_memcpy(&v[j], q + 16 * j, 16);  // unaligned global_load_dwordx4
 }
 
+// The chunk's digest into its slot and, when the caller keeps a dense fingerprint table, its
+// 48-byte record {digest[32], u64 buffer id, u32 start, u32 len} at rec_base[b] + k.
+template <int ALGO>
+__device__ __forceinline__ void store_digest(const HashArgs& a, uint32_t slot, uint32_t b, uint32_t k, uint32_t cs,
+                                             uint32_t len, const uint32_t (&s)[8]) {
+    constexpr bool SHA = ALGO != 2;
+    uint32_t dig[8];
+    if constexpr (SHA) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) dig[j] = __builtin_bswap32(s[j]);
+        if constexpr (ALGO == 1) dig[5] = dig[6] = dig[7] = 0;  // VARIABLE_SHA256_160: first 20 bytes
+    } else {
+        dig[0] = s[0]; dig[1] = s[1]; dig[2] = s[2]; dig[3] = s[3];
+        dig[4] = dig[5] = dig[6] = dig[7] = 0;
+    }
+    uint4* out = reinterpret_cast<uint4*>(a.digests + (uint64_t)slot * 32);
+    const uint4 d0 = make_uint4(dig[0], dig[1], dig[2], dig[3]);
+    const uint4 d1 = make_uint4(dig[4], dig[5], dig[6], dig[7]);
+    out[0] = d0;
+    out[1] = d1;
+    if (a.records) {
+        const uint64_t r = (uint64_t)a.rec_base[b] + k;
+        if (r < a.records_cap) {
+            uint4* rec = reinterpret_cast<uint4*>(a.records + r * kRecordBytes);
+            const uint64_t id = a.buffer_id_base + b;
+            rec[0] = d0;
+            rec[1] = d1;
+            rec[2] = make_uint4((uint32_t)id, (uint32_t)(id >> 32), cs, len);
+        }
+    }
+}
+
 // ABL (sweep builds only): 1 = synthesize the message words instead of loading them, 2 = skip the
 // compression (fold the loaded words instead), 4 = read from the chunk start rounded down to 128 B
 // (wrong digests; every line is fetched once: the cost of the unaligned-line re-fetch).
@@ -819,30 +851,7 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
             s[0] = m4[0]; s[1] = m4[1]; s[2] = m4[2]; s[3] = m4[3];
         }
     }
-    uint32_t dig[8];
-    if constexpr (SHA) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) dig[j] = __builtin_bswap32(s[j]);
-        if constexpr (ALGO == 1) dig[5] = dig[6] = dig[7] = 0;  // VARIABLE_SHA256_160: first 20 bytes
-    } else {
-        dig[0] = s[0]; dig[1] = s[1]; dig[2] = s[2]; dig[3] = s[3];
-        dig[4] = dig[5] = dig[6] = dig[7] = 0;
-    }
-    uint4* out = reinterpret_cast<uint4*>(a.digests + (uint64_t)slot * 32);
-    const uint4 d0 = make_uint4(dig[0], dig[1], dig[2], dig[3]);
-    const uint4 d1 = make_uint4(dig[4], dig[5], dig[6], dig[7]);
-    out[0] = d0;
-    out[1] = d1;
-    if (a.records) {
-        const uint64_t r = (uint64_t)a.rec_base[b] + k;
-        if (r < a.records_cap) {
-            uint4* rec = reinterpret_cast<uint4*>(a.records + r * kRecordBytes);
-            const uint64_t id = a.buffer_id_base + b;
-            rec[0] = d0;
-            rec[1] = d1;
-            rec[2] = make_uint4((uint32_t)id, (uint32_t)(id >> 32), cs, len);
-        }
-    }
+    store_digest<ALGO>(a, slot, b, k, cs, len, s);
 }
 
 // PRIO: a wave whose chunks are long raises its issue priority.  A chunk's SHA-256 is a serial
@@ -870,7 +879,7 @@ void chunk_hash_kernel(HashArgs a) {
 // Persistent form: a fixed grid (a.persist_grid workgroups) whose waves take the next 64 tasks
 // of the longest-first list from a counter until it runs dry.  A capped grid leaves register
 // room on every CU for a concurrently running scan (a.wave_ctr is zeroed by the caller).
-template <int ALGO, bool PF>
+template <int ALGO, bool PF, int ABL = 0>
 __global__ __launch_bounds__(256) void chunk_hash_persistent_kernel(HashArgs a) {
     const uint32_t total = *a.total;
     const uint32_t lane = threadIdx.x & 63;
@@ -879,8 +888,130 @@ __global__ __launch_bounds__(256) void chunk_hash_persistent_kernel(HashArgs a) 
         if (lane == 0) base = atomicAdd(a.wave_ctr, 64u);
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         if (base >= total) break;
-        if (base + lane < total) hash_task<ALGO, 0, PF>(a, base + lane);
+        if (base + lane < total) hash_task<ALGO, ABL, PF>(a, base + lane);
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// 5b. latency form of the fingerprint (small batches: a coalescing-queue pass costs its longest
+//     chunk's serial SHA-256 chain).  A 128-thread workgroup takes 64 chunks
+//     (longest first, as above); wave 0 builds each 64-byte block's message schedule W[t] + K[t]
+//     into LDS one block ahead of wave 1, which runs only the 64 rounds.  A wave alone on its
+//     SIMD issues one VALU instruction per ~4 cycles, so the chain's wave issues ~920 instead of
+//     ~1 423 instructions per block.  Same digests as chunk_hash_kernel (SHA-256 / SHA-256/160).
+// ------------------------------------------------------------------------------------------
+constexpr int kSplitTasks = 64;  // chunks per workgroup (one per lane of each wave)
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t x = __shfl_xor(v, o);
+        v = x > v ? x : v;
+    }
+    return v;
+}
+
+template <int ALGO>
+__global__ __launch_bounds__(128) void chunk_hash_split_kernel(HashArgs a) {
+    static_assert(ALGO != 2, "MD5 has no split form");
+    __shared__ uint4 wk[2][16][kSplitTasks];  // [buffer][t / 4][lane] = W[t..t+3] + K[t..t+3]
+    const uint32_t lane = threadIdx.x & 63;
+    const bool producer = threadIdx.x < 64;
+    const uint32_t i = blockIdx.x * kSplitTasks + lane;
+    const uint32_t ntask = *a.total;
+    uint32_t slot = 0, b = 0, k = 0, cs = 0, len = 0, nfull = 0, nblocks = 0;
+    const uint8_t* p = a.zero_page;
+    if (i < ntask) {
+        slot = a.tasks[i];
+        b = slot / a.cap;
+        k = slot - b * a.cap;
+        const uint64_t boff = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
+        cs = a.starts[slot];
+        len = a.clens[slot];
+        p = a.data + boff + cs;
+        nfull = len >> 6;
+        nblocks = (len + 8) / 64 + 1;
+    }
+    const uint32_t maxnb = wave_max_u32(nblocks);  // identical in both waves (same 64 tasks)
+    if (blockIdx.x * kSplitTasks >= ntask) return;  // whole workgroup past the end (uniform)
+    uint32_t s[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint4 nx[4];
+    if (producer) load_block64(nx, nfull ? p : a.zero_page);
+    for (uint32_t it = 0; it <= maxnb; it++) {
+        if (producer) {
+            if (it < maxnb) {
+                const uint32_t blk = it;
+                uint4 cur[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) cur[q] = nx[q];
+                load_block64(nx, blk + 1 < nfull ? p + 64 * (blk + 1) : a.zero_page);
+                if (blk < nblocks) {
+                    uint32_t w[16];
+                    if (blk < nfull) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            w[4 * q] = __builtin_bswap32(cur[q].x);
+                            w[4 * q + 1] = __builtin_bswap32(cur[q].y);
+                            w[4 * q + 2] = __builtin_bswap32(cur[q].z);
+                            w[4 * q + 3] = __builtin_bswap32(cur[q].w);
+                        }
+                    } else {
+                        if (blk == nfull) {
+                            tail_words<true>(w, p + 64 * nfull, len & 63);
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 16; j++) w[j] = 0;
+                        }
+                        if (blk == nblocks - 1) {
+                            const uint64_t bits = (uint64_t)len * 8;
+                            w[14] = (uint32_t)(bits >> 32);
+                            w[15] = (uint32_t)bits;
+                        }
+                    }
+                    uint4(*dst)[kSplitTasks] = wk[blk & 1];
+#pragma unroll
+                    for (int g = 0; g < 16; g++) {
+                        if (g >= 4 && (g & 3) == 0) {
+                            // W[16g' .. 16g'+15] in place over the 16-word window
+#pragma unroll
+                            for (int j = 0; j < 16; j++) {
+                                const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+                                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                                w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+                            }
+                        }
+                        const int t = 4 * g;
+                        dst[g][lane] = make_uint4(w[t & 15] + kSha256K[t], w[(t + 1) & 15] + kSha256K[t + 1],
+                                                  w[(t + 2) & 15] + kSha256K[t + 2], w[(t + 3) & 15] + kSha256K[t + 3]);
+                    }
+                }
+            }
+        } else if (it >= 1) {
+            const uint32_t blk = it - 1;
+            if (blk < nblocks) {
+                const uint4(*src)[kSplitTasks] = wk[blk & 1];
+                uint32_t a0 = s[0], b0 = s[1], c0 = s[2], d0 = s[3], e0 = s[4], f0 = s[5], g0 = s[6], h0 = s[7];
+#pragma unroll
+                for (int g = 0; g < 16; g++) {
+                    const uint4 q = src[g][lane];
+                    const uint32_t wkv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t S1 = xor3(rotr(e0, 6), rotr(e0, 11), rotr(e0, 25));
+                        const uint32_t ch = (e0 & f0) | (~e0 & g0);
+                        const uint32_t t1 = h0 + S1 + ch + wkv[r];
+                        const uint32_t S0 = xor3(rotr(a0, 2), rotr(a0, 13), rotr(a0, 22));
+                        const uint32_t mj = maj3(a0, b0, c0);
+                        h0 = g0; g0 = f0; f0 = e0; e0 = d0 + t1; d0 = c0; c0 = b0; b0 = a0; a0 = t1 + S0 + mj;
+                    }
+                }
+                s[0] += a0; s[1] += b0; s[2] += c0; s[3] += d0; s[4] += e0; s[5] += f0; s[6] += g0; s[7] += h0;
+            }
+        }
+        __syncthreads();
+    }
+    if (!producer && i < ntask) store_digest<ALGO>(a, slot, b, k, cs, len, s);
 }
 
 }  // namespace sdfs

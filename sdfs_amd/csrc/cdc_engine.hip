@@ -217,6 +217,7 @@ struct sdfs_cdc_engine {
     int hash_variant = 0;
     int hash_wg_per_cu = 2;
     uint32_t scan_max_block = kScanThreads;  // widest scan workgroup (tuning build: SDFS_SCAN_MAX_BLOCK)
+    bool hash_split = true;                  // latency form of the fingerprint for small batches (tuning: SDFS_HASH_SPLIT)
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
@@ -511,7 +512,14 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     ha.persist_grid = (uint32_t)(e->num_cus * e->hash_wg_per_cu);
     {
         const int t = t_begin(e, K_HASH, s);
-        HIP_TRY(launch_hash(ha, (uint64_t)nbuf * out->cap, e->hash_variant, s));
+        const uint64_t max_tasks = (uint64_t)nbuf * out->cap;
+        // a batch too small to give every SIMD a wave (a coalescing-queue pass) costs its longest
+        // chunk's serial chain: the two-wave latency form shortens it
+        if (e->hash_split && e->prm.hash_algo != SDFS_CDC_MD5 && e->hash_variant == 0 &&
+            max_tasks <= (uint64_t)e->num_cus * 128)
+            HIP_TRY(launch_hash_split(ha, max_tasks, s));
+        else
+            HIP_TRY(launch_hash(ha, max_tasks, e->hash_variant, s));
         t_end(e, t, s);
     }
     t_end(e, tpipe, s);
@@ -831,6 +839,9 @@ struct QueueBackend {
         HIP_TRY(w.x_scratch.ensure(kExtentScratchWords + 2ull * max_reqs));
         HIP_TRY(hipEventCreateWithFlags(&d->kdone, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&d->ws.free_ev, hipEventDisableTiming));
+        // touch the pinned staging once here, not inside some caller's first request
+        memset(s.in, 0, slot_bytes);
+        memset(d->pin_out, 0, d->pin_out_n);
         return SDFS_CDC_OK;
     }
 
@@ -990,6 +1001,10 @@ bool queue_ready(sdfs_cdc_engine* e) {
         e->q_state = -1;
         return false;
     }
+    // first work on a stream sets up its hardware queue (milliseconds): do it for every lane now
+    for (hipStream_t st : e->qs)
+        if (hipMemsetAsync(e->zero_page.p, 0, 256, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+            (void)hipGetLastError();
     e->q_state = 1;
     return true;
 }
@@ -1074,6 +1089,7 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     if (const char* v = getenv("SDFS_SEG_LEN")) e->seg_len = (uint32_t)atoi(v);
     if (const char* v = getenv("SDFS_HASH_VARIANT")) e->hash_variant = atoi(v);
     if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
+    if (const char* v = getenv("SDFS_HASH_SPLIT")) e->hash_split = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif

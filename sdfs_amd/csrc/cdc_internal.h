@@ -157,6 +157,8 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);
 hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);
+// latency form for small batches (SHA-256 / SHA-256/160 only): two waves per 64 chunks
+hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t stream);
 hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t stream);
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
                         hipStream_t stream);

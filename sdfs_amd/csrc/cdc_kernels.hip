@@ -525,6 +525,17 @@ hipError_t launch_scatter(const ScatterArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t s) {
+    const uint32_t blocks = (uint32_t)((max_tasks + kSplitTasks - 1) / kSplitTasks);
+    if (blocks == 0) return hipSuccess;
+    switch (a.algo) {
+    case 0: hipLaunchKernelGGL((chunk_hash_split_kernel<0>), dim3(blocks), dim3(128), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((chunk_hash_split_kernel<1>), dim3(blocks), dim3(128), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t s) {
     const uint32_t blocks = (uint32_t)((max_tasks + 255) / 256);
     if (blocks == 0) return hipSuccess;

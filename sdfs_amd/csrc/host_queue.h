@@ -128,6 +128,8 @@ struct QReq {
     int slot = -1;
     uint32_t idx = 0;   // index among the slot's requests of its kind
     uint64_t off = 0;   // staging offset of its bytes
+    // admission (set by the queue for a caller that waited for room: 1 = placed, < 0 = refused)
+    int admit = 0;
     // completion
     int status = 0;
     bool done = false;
@@ -229,6 +231,7 @@ class CoalescingQueue {
         }
         cv_disp_.notify_all();
         for (auto& cv : comp_cv_) cv.notify_all();
+        for (auto& cv : cv_admit_) cv.notify_all();
         if (disp_.joinable()) disp_.join();
         for (auto& t : comp_)
             if (t.joinable()) t.join();
@@ -245,74 +248,34 @@ class CoalescingQueue {
     int run(QReq& r, ReadFn&& read) {
         std::unique_lock<std::mutex> lk(m_);
         if (!prepared_ || stop_) return kQueueStopped;
-        const uint64_t need = r.kind == QReq::kChunks ? qalign(r.len, 64) : qalign(r.len, 16);
         if (r.len > max_req_) return kQueueTooBig;  // callers check accepts() first
         active_++;
-        QSlot* s = nullptr;
-        for (;;) {
-            if (open_ >= 0) {
-                QSlot& o = slots_[open_];
-                if (o.nreq() < c_.max_reqs && o.lo + need <= o.hi && b_.admits(o, r)) {
-                    s = &o;
-                    break;
-                }
-                if (o.nreq() == 0) {  // not even an empty slot takes it
-                    active_--;
-                    return kQueueTooBig;
-                }
-                o.full = true;  // launch it without lingering
-            }
-            if (open_ < 0) {  // open a free slot
-                for (size_t i = 0; i < slots_.size(); i++)
-                    if (slots_[i].state == QSlot::kFree) {
-                        QSlot& f = slots_[i];
-                        f.state = QSlot::kOpen;
-                        f.lo = 0;
-                        f.hi = f.cap;
-                        f.chunks.clear();
-                        f.hashes.clear();
-                        f.uniform_len = 0;
-                        f.max_chunk_len = 0;
-                        f.copying = f.readers = 0;
-                        f.status = 0;
-                        f.full = false;
-                        f.seq = ++seq_;
-                        f.t_open = std::chrono::steady_clock::now();
-                        open_ = (int)i;
+        // Admission is first come, first served: a caller that finds no room joins the waiting
+        // line, and whoever makes room (a slot launched or freed) places the waiting requests in
+        // arrival order while they fit, then wakes their callers.  (Waking every waiter to race
+        // for the room let an unlucky caller lose for several passes: 8-10 ms tails.)
+        int rc = waitq_.empty() ? place(r) : 0;
+        if (rc == 0) {
+            r.admit = 0;
+            waitq_.push_back(&r);
+            cv_disp_.notify_one();  // the open slot is full: have it launched
+            admit_cv(&r).wait(lk, [&] { return r.admit != 0 || stop_; });
+            if (r.admit == 0) {  // stopped while waiting
+                for (auto it = waitq_.begin(); it != waitq_.end(); ++it)
+                    if (*it == &r) {
+                        waitq_.erase(it);
                         break;
                     }
-                if (open_ >= 0) continue;
-            }
-            // the open slot is full (the dispatcher launches it as soon as a lane is idle) or
-            // every slot is busy: wait for space
-            cv_disp_.notify_one();
-            cv_space_.wait(lk);
-            if (stop_) {
                 active_--;
                 return kQueueStopped;
             }
+            rc = r.admit;
         }
-        r.slot = open_;
-        r.done = false;
-        r.status = 0;
-        if (r.kind == QReq::kChunks) {
-            r.off = s->lo;
-            s->lo += need;
-            r.idx = (uint32_t)s->chunks.size();
-            if (s->chunks.empty())
-                s->uniform_len = (uint32_t)r.len;
-            else if (s->uniform_len != r.len)
-                s->uniform_len = 0;
-            if (r.len > s->max_chunk_len) s->max_chunk_len = r.len;
-            s->chunks.push_back(&r);
-        } else {
-            s->hi -= need;
-            r.off = s->hi;
-            r.idx = (uint32_t)s->hashes.size();
-            s->hashes.push_back(&r);
+        if (rc != 1) {  // not even an empty slot takes it
+            active_--;
+            return kQueueTooBig;
         }
-        if (s->nreq() >= c_.max_reqs || s->hi - s->lo < max_req_) s->full = true;
-        s->copying++;
+        QSlot* s = &slots_[r.slot];
         cv_disp_.notify_one();
         lk.unlock();
         if (r.len) memcpy(s->in + r.off, r.src, r.len);
@@ -320,14 +283,14 @@ class CoalescingQueue {
         if (--s->copying == 0) cv_disp_.notify_all();
         done_cv_[r.slot].wait(lk, [&] { return r.done; });  // woken with its own slot only
         lk.unlock();
-        const int rc = read(*s, r, r.status);
+        const int ret = read(*s, r, r.status);
         lk.lock();
         active_--;
         if (--s->readers == 0) {
             s->state = QSlot::kFree;
-            cv_space_.notify_all();
+            admit_waiting();
         }
-        return rc;
+        return ret;
     }
 
     // statistics (tests, bench)
@@ -350,6 +313,81 @@ class CoalescingQueue {
     }
 
   private:
+    std::condition_variable& admit_cv(const QReq* q) {
+        return cv_admit_[(reinterpret_cast<uintptr_t>(q) >> 6) % kAdmitCvs];
+    }
+
+    // Places `r` in the open slot, opening a free slot when there is none (queue lock held).
+    // 1 = placed (the caller copies its bytes to s.in + r.off next), 0 = no room now (the open
+    // slot is marked full so that it launches), kQueueTooBig = not even an empty slot takes it.
+    int place(QReq& r) {
+        const uint64_t need = r.kind == QReq::kChunks ? qalign(r.len, 64) : qalign(r.len, 16);
+        if (open_ < 0) {
+            for (size_t i = 0; i < slots_.size() && open_ < 0; i++)
+                if (slots_[i].state == QSlot::kFree) {
+                    QSlot& f = slots_[i];
+                    f.state = QSlot::kOpen;
+                    f.lo = 0;
+                    f.hi = f.cap;
+                    f.chunks.clear();
+                    f.hashes.clear();
+                    f.uniform_len = 0;
+                    f.max_chunk_len = 0;
+                    f.copying = f.readers = 0;
+                    f.status = 0;
+                    f.full = false;
+                    f.seq = ++seq_;
+                    f.t_open = std::chrono::steady_clock::now();
+                    open_ = (int)i;
+                }
+            if (open_ < 0) return 0;  // every slot is busy
+        }
+        QSlot& o = slots_[open_];
+        if (!(o.nreq() < c_.max_reqs && o.lo + need <= o.hi && b_.admits(o, r))) {
+            if (o.nreq() == 0) return kQueueTooBig;
+            o.full = true;  // launch it without lingering
+            return 0;
+        }
+        r.slot = open_;
+        r.done = false;
+        r.status = 0;
+        if (r.kind == QReq::kChunks) {
+            r.off = o.lo;
+            o.lo += need;
+            r.idx = (uint32_t)o.chunks.size();
+            if (o.chunks.empty())
+                o.uniform_len = (uint32_t)r.len;
+            else if (o.uniform_len != r.len)
+                o.uniform_len = 0;
+            if (r.len > o.max_chunk_len) o.max_chunk_len = r.len;
+            o.chunks.push_back(&r);
+        } else {
+            o.hi -= need;
+            r.off = o.hi;
+            r.idx = (uint32_t)o.hashes.size();
+            o.hashes.push_back(&r);
+        }
+        if (o.nreq() >= c_.max_reqs || o.hi - o.lo < max_req_) o.full = true;
+        o.copying++;
+        return 1;
+    }
+
+    // Room may have appeared (a slot launched or freed): place waiting requests in arrival order
+    // while they fit and wake their callers (queue lock held).
+    void admit_waiting() {
+        bool any = false;
+        while (!waitq_.empty()) {
+            QReq* q = waitq_.front();
+            const int rc = place(*q);
+            if (rc == 0) break;
+            waitq_.pop_front();
+            q->admit = rc;
+            admit_cv(q).notify_all();
+            any = true;
+        }
+        if (any) cv_disp_.notify_one();
+    }
+
     // Whether the open slot should go now (queue lock held); else *deadline = when it will.
     bool ready(std::chrono::steady_clock::time_point* deadline) {
         if (open_ < 0 || inflight_ >= c_.lanes) return false;
@@ -389,7 +427,7 @@ class CoalescingQueue {
             for (int l = 1; l < c_.lanes; l++)
                 if (lane_busy_[l] < lane_busy_[lane]) lane = l;
             lane_busy_[lane]++;
-            cv_space_.notify_all();  // waiting callers may open the next slot now
+            admit_waiting();  // waiting callers may open the next slot now
             cv_disp_.wait(lk, [&] { return s.copying == 0; });
             s.readers = (int)s.nreq();
             launched_++;
@@ -445,7 +483,12 @@ class CoalescingQueue {
     Config c_;
     std::vector<QSlot> slots_;
     std::mutex m_;
-    std::condition_variable cv_disp_, cv_space_;
+    // callers waiting for room, in arrival order; each waits on a condition variable picked by
+    // its request's address, so an admission wakes (about) one thread, not every waiting caller
+    static constexpr uintptr_t kAdmitCvs = 64;
+    std::deque<QReq*> waitq_;
+    std::condition_variable cv_admit_[kAdmitCvs];
+    std::condition_variable cv_disp_;
     std::vector<std::condition_variable> done_cv_;  // per slot: its callers wait for its batch
     std::vector<std::deque<QSlot*>> flight_;        // per lane, in launch order
     std::vector<std::condition_variable> comp_cv_;  // per lane

@@ -496,3 +496,36 @@ def test_pinned_host_batch_direct_copy_matches_pageable():
     finally:
         _lib.check(_lib.load().sdfs_cdc_host_unregister(reg.ctypes.data))
     e.destroy()
+
+
+@pytest.mark.parametrize("algo", [O.SHA256, O.SHA256_160])
+def test_small_batch_latency_form_equals_throughput_form(algo):
+    """Batches too small to fill the GPU fingerprint with the two-wave latency kernel
+    (chunk_hash_split_kernel: message schedule and rounds in separate waves); larger ones with
+    the one-lane-per-chunk kernel.  The same buffers through both sizes give identical records,
+    and the small batch equals the oracle, including maxLen chunks (long zero-free runs with no
+    candidate) and dense-candidate buffers."""
+    prm = P(hash_algo=algo)
+    e = engine_for(prm)
+    buf_len = 262144
+    host = _dense_candidate_buffers(32, buf_len)
+    host[7] = 0xFF  # no candidate anywhere: maxLen chunks
+    host[9, 100000:200000] = 0x55  # a candidate-free stretch inside random data
+    small = DeviceBatch(e, nbuf=32, buf_len=buf_len)  # 32 x cap tasks: latency form
+    small.data.copy_(torch.from_numpy(host.reshape(-1)))
+    small.run()
+    big = DeviceBatch(e, nbuf=1024, buf_len=buf_len)  # 1024 x cap tasks: throughput form
+    big.fill_streams(first_stream=5, bufs_per_stream=256)
+    big.data[: 32 * buf_len].copy_(small.data)
+    big.run()
+    cs, ss, ls, ds, _ = small.host_results()
+    cb, sb, lb, db, _ = big.host_results()
+    assert (cs == cb[:32]).all()
+    assert (ss == sb[:32]).all() and (ls == lb[:32]).all() and (ds == db[:32]).all()
+    dl = O.Params(**prm).digest_len
+    for b in list(range(0, 32, 3)) + [7]:
+        es, el, ed = O.chunk(host[b].tobytes(), O.Params(**prm))
+        c = cs[b]
+        assert ss[b, :c].tolist() == es.tolist() and ls[b, :c].tolist() == el.tolist(), b
+        assert (ds[b, :c, :dl] == ed).all(), b
+    assert int(ls.max()) == prm["max_len"]  # a full maxLen chain went through the latency form
