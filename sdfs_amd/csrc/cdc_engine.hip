@@ -218,6 +218,7 @@ struct sdfs_cdc_engine {
     int hash_wg_per_cu = 2;
     uint32_t scan_max_block = kScanThreads;  // widest scan workgroup (tuning build: SDFS_SCAN_MAX_BLOCK)
     bool hash_split = true;                  // latency form of the fingerprint for small batches (tuning: SDFS_HASH_SPLIT)
+    bool small_seg = true;                   // short scan segments for small batches (tuning: SDFS_SMALL_SEG)
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
@@ -378,6 +379,13 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
         if (e->run) e->runs_recorded++;
         return SDFS_CDC_OK;
     }
+    // A batch of fewer buffers than SIMDs (a coalescing-queue pass) scans in short segments: the
+    // fused walk's one wave per buffer would leave most SIMDs idle and put a 4 KiB serial chain on
+    // every lane (0.18 ms); 512-byte segments plus the separate walk take ~0.07 ms.
+    const uint32_t seg_len = (nbuf < (uint32_t)e->num_cus * 4 && e->seg_len > kSmallBatchSeg &&
+                              e->seg_len % kSmallBatchSeg == 0 && e->small_seg)
+                                 ? kSmallBatchSeg
+                                 : e->seg_len;
     uint32_t* hist = w->small.p;
     uint32_t* cursor = w->small.p + kMaxBins;
     uint32_t* total = w->small.p + 2 * kMaxBins + 1;
@@ -385,7 +393,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
         const int t = t_begin(e, K_PREP, s);
         HIP_TRY(hipMemsetAsync(w->small.p, 0, (kSmall + 8) * sizeof(uint32_t), s));
         if (ovf_to) HIP_TRY(hipMemsetAsync(ovf_to, 0, sizeof(uint32_t), s));
-        if (!uniform_len) HIP_TRY(launch_seg_prefix(d_lens, nbuf, e->seg_len, w->seg_prefix.p, s));
+        if (!uniform_len) HIP_TRY(launch_seg_prefix(d_lens, nbuf, seg_len, w->seg_prefix.p, s));
         t_end(e, t, s);
     }
     const bool pred64 = (e->prm.pred_mask >> 32) != 0;
@@ -396,7 +404,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     sa.bitmap = w->bitmap.p;
     sa.nbuf = nbuf;
     sa.uniform_len = uniform_len;
-    sa.seg_len = e->seg_len;
+    sa.seg_len = seg_len;
     sa.jshift = (uint32_t)(e->degree - 40);
     sa.mask_lo = (uint32_t)e->prm.pred_mask;
     sa.mask_hi = (uint32_t)(e->prm.pred_mask >> 32);
@@ -406,12 +414,12 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     sa.zero_page = e->zero_page.p;
     uint64_t seg_bound;
     if (uniform_len) {
-        const uint64_t spb = (uniform_len + e->seg_len - 1) / e->seg_len;
+        const uint64_t spb = (uniform_len + seg_len - 1) / seg_len;
         sa.total_segs = spb * nbuf;
         seg_bound = sa.total_segs;
     } else {
         sa.seg_prefix = w->seg_prefix.p;
-        seg_bound = data_bytes / e->seg_len + nbuf;
+        seg_bound = data_bytes / seg_len + nbuf;
     }
     ResolveArgs ra{};
     ra.bitmap = w->bitmap.p;
@@ -440,7 +448,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     }
     // one wave = one buffer: the scan kernel resolves the cuts in its epilogue
     const bool fused = e->scan_info.fuse && uniform_len && e->scan_info.chains == 1 &&
-                       (uint64_t)uniform_len == 64ull * e->seg_len && e->seg_len < 0xFFFFu;
+                       (uint64_t)uniform_len == 64ull * seg_len && seg_len < 0xFFFFu;
     sa.fuse_resolve = fused ? 1u : 0u;
     sa.res = ra;
     // One workgroup per CU (the LDS tables); a batch too small to give every CU 1024 threads
@@ -1090,6 +1098,7 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     if (const char* v = getenv("SDFS_HASH_VARIANT")) e->hash_variant = atoi(v);
     if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_HASH_SPLIT")) e->hash_split = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SMALL_SEG")) e->small_seg = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif

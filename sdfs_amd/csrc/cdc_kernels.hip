@@ -423,8 +423,9 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     uint32_t blocks = (a.nbuf + 3) / 4;
-    // a few buffers per wave so the per-block histogram flush is amortised
-    blocks = (blocks + 3) / 4;
+    // large batches: a few buffers per wave so the per-block histogram flush is amortised; small
+    // ones (a queue pass) one buffer per wave, since each walk is a serial chain of bitmap loads
+    if (a.nbuf > 4096) blocks = (blocks + 3) / 4;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(cdc_resolve_kernel, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
