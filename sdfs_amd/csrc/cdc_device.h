@@ -108,6 +108,41 @@ __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& 
         cand_shift<PRED64>(bits, lo, hi, a);
 }
 
+// Byte O of every chain at once (NCH > 1): all chains' lookup addresses and their 2 x NCH LDS
+// reads first, then each chain's update, so the chains' lookup latencies overlap (hipcc's
+// waitcnt pass then waits lgkmcnt(2 x later chains) before each chain's update).  The reads are
+// volatile so that they stay in issue order ahead of the updates: left alone, hipcc reuses one
+// destination pair for every chain and waits lgkmcnt(0) per chain.
+template <int W, bool PRED64, int O, int NCH, int BLKW>
+__device__ __forceinline__ void bytes_multi(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
+                                            const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
+                                            uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
+    constexpr int OLD = O - W;
+    constexpr int OI = OLD >= 0 ? OLD : OLD + 64;
+    constexpr int Q = OI & 3;
+    uint2 pv[NCH], qv[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const uint32_t odw = OLD >= 0 ? cur[c][OI >> 2] : prev[c][OI >> 2];
+        const uint32_t pa = bitop3_and_or(hi[c] >> (a.jshift - 8), 0xFF00u, push_base);
+        const uint32_t qa = __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + Q) << 8));
+        typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
+        const __attribute__((address_space(3))) uint8_t* lt = (const __attribute__((address_space(3))) uint8_t*)tab;
+        const uint64_t pw = *(lds_u64*)(lt + pa);
+        const uint64_t qw = *(lds_u64*)(lt + qa);
+        pv[c] = make_uint2((uint32_t)pw, (uint32_t)(pw >> 32));
+        qv[c] = make_uint2((uint32_t)qw, (uint32_t)(qw >> 32));
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const uint32_t nhi = __builtin_amdgcn_alignbit(hi[c], lo[c], 24);
+        const uint32_t nlo = __builtin_amdgcn_perm(lo[c], cur[c][O >> 2], 0x06050400u | (O & 3));
+        lo[c] = xor3(nlo, pv[c].x, qv[c].x);
+        hi[c] = xor3(nhi, pv[c].y, qv[c].y);
+        cand_shift<PRED64>(bits[c], lo[c], hi[c], a);
+    }
+}
+
 #ifndef SDFS_SCAN_SCHED_GROUP
 #define SDFS_SCAN_SCHED_GROUP 4
 #endif
@@ -120,12 +155,18 @@ __device__ __forceinline__ void word_steps(uint32_t (&lo)[NCH], uint32_t (&hi)[N
                                            const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
                                            uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
     if constexpr (O < O0 + 32) {
+        if constexpr (NCH > 1 && ABL == 0) {
+            bytes_multi<W, PRED64, O, NCH, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+        } else {
 #pragma unroll
-        for (int c = 0; c < NCH; c++)
-            byte_step<W, PRED64, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
-        // keep the scheduler from hoisting every (chain-independent) pop read of the block
-        // ahead of the rolling chain: that costs ~2 VGPRs per byte and spills.
-        if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) __builtin_amdgcn_sched_barrier(0);
+            for (int c = 0; c < NCH; c++)
+                byte_step<W, PRED64, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
+        }
+        if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) {
+            // keep the scheduler from hoisting every (chain-independent) pop read of the block
+            // ahead of the rolling chain: that costs ~2 VGPRs per byte and spills.
+            __builtin_amdgcn_sched_barrier(0);
+        }
         word_steps<W, PRED64, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
     }
 }
@@ -392,9 +433,14 @@ __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint3
 // (sweep only, measured slower); 2 = each lane keeps its segment's first kSumCands candidate
 // offsets in registers while it scans, and the wave resolves its buffer from them in the epilogue
 // (no bitmap reads unless a segment overflows: DESIGN.md §4).
-template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64, int FUSE = 0>
+// THREADS: the widest workgroup the variant is launched with (the register budget follows from
+// THREADS and WPS: 512 / waves-per-SIMD VGPRs, so 768 threads at 3 waves/SIMD allow 168).
+// With FUSE 2 and two chains, chain c of a wave covers segments base + c * blockDim.x + 64w ..
+// + 63, i.e. its own buffer, and the epilogue walks both buffers.
+template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64, int FUSE = 0, int THREADS = kScanThreads>
 struct ScanCfg {
-    static constexpr int kFuse = NCH == 1 ? FUSE : 0;  // resolve each wave's buffer in the epilogue
+    static constexpr int kFuse = NCH == 1 ? FUSE : (FUSE == 2 ? 2 : 0);  // resolve each wave's buffer(s) in the epilogue
+    static constexpr int kThreads = THREADS;
     static constexpr int kAbl = ABL;
     static constexpr int kCopies = C;
     static constexpr int kChains = NCH;
@@ -406,7 +452,7 @@ struct ScanCfg {
 };
 
 template <int W, bool PRED64, class CFG>
-__global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
+__global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
     constexpr int NCH = CFG::kChains;
     constexpr int C = CFG::kCopies;
     constexpr int BLK = CFG::kBlk;
@@ -472,9 +518,15 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
         uint32_t lo[NCH], hi[NCH];
         uint32_t prev[NCH][16], cur[NCH][BLKW];
         bool cur_full[NCH];
-        uint32_t sm[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};  // FUSE == 2: candidate summary
-        uint32_t ncand = 0;
-        uint32_t ovf_off = 0xFFFFFFFFu;  // FUSE == 2: segment offset of the first stored bitmap block
+        uint32_t sm[NCH][4];  // FUSE == 2: candidate summary per chain
+        uint32_t ncand[NCH];
+        uint32_t ovf_off[NCH];  // FUSE == 2: segment offset of the first stored bitmap block
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            sm[c][0] = sm[c][1] = sm[c][2] = sm[c][3] = 0xFFFFFFFFu;
+            ncand[c] = 0;
+            ovf_off[c] = 0xFFFFFFFFu;
+        }
         // FUSE == 2 with the fused resolve: bitmap words are stored only once a lane's summary has
         // overflowed (> kSumCands candidates), from that block on; resolve_from_summary reads them
         // only there.  Saves the 0.5 GB of bitmap writes per 4 GiB.
@@ -544,20 +596,22 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
             if constexpr (CFG::kFuse == 2) {
                 // candidates are rare (~1 per 4 KiB): a divergent, seldom-taken append
 #pragma unroll
-                for (int w = 0; w < BLK / 32; w++) {
-                    uint32_t bits = blk < nblk[0] ? words[0][w] : 0u;
-                    while (bits) {
-                        const uint32_t off = blk * BLK + 32 * w + __builtin_ctz(bits);
-                        bits &= bits - 1;
-                        if (start[0] + off < end[0]) sum_push(sm, ncand, off);
+                for (int c = 0; c < NCH; c++)
+#pragma unroll
+                    for (int w = 0; w < BLK / 32; w++) {
+                        uint32_t bits = blk < nblk[c] ? words[c][w] : 0u;
+                        while (bits) {
+                            const uint32_t off = blk * BLK + 32 * w + __builtin_ctz(bits);
+                            bits &= bits - 1;
+                            if (start[c] + off < end[c]) sum_push(sm[c], ncand[c], off);
+                        }
                     }
-                }
             }
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 if constexpr (CFG::kFuse == 2)
-                    if (ncand > kSumCands && ovf_off == 0xFFFFFFFFu) ovf_off = blk * BLK;
-                if (blk < nblk[c] && (!sparse_bm || ncand > kSumCands)) {
+                    if (ncand[c] > kSumCands && ovf_off[c] == 0xFFFFFFFFu) ovf_off[c] = blk * BLK;
+                if (blk < nblk[c] && (!sparse_bm || ncand[c] > kSumCands)) {
                     const uint64_t pos = start[c] + (uint64_t)BLK * blk;
                     uint32_t* bm = a.bitmap + (pos >> 5);
                     if (pos + BLK <= end[c]) {
@@ -593,8 +647,13 @@ __global__ __launch_bounds__(kScanThreads, CFG::kWavesPerSimd) void cdc_scan_ker
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 if constexpr (CFG::kFuse == 2) {
-                    if (seg0 < total)
-                        resolve_from_summary(a.res, (uint32_t)(seg0 >> 6), lane, sm, ncand, ovf_off, a.seg_len, lhist);
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) {
+                        const uint64_t sc = seg0 + (uint64_t)c * blockDim.x;
+                        if (sc < total)
+                            resolve_from_summary(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c], ovf_off[c], a.seg_len,
+                                                 lhist);
+                    }
                 } else {
                     if (seg0 < total) resolve_buffer(a.res, (uint32_t)(seg0 >> 6), lane, lhist);
                 }

@@ -447,7 +447,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
         ra.spec_next = w->spec_next.p;
     }
     // one wave = one buffer: the scan kernel resolves the cuts in its epilogue
-    const bool fused = e->scan_info.fuse && uniform_len && e->scan_info.chains == 1 &&
+    const bool fused = e->scan_info.fuse && uniform_len && (e->scan_info.chains == 1 || e->scan_info.fuse == 2) &&
                        (uint64_t)uniform_len == 64ull * seg_len && seg_len < 0xFFFFu;
     sa.fuse_resolve = fused ? 1u : 0u;
     sa.res = ra;
@@ -457,7 +457,8 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     const uint64_t max_wgs = (uint64_t)e->num_cus * e->scan_info.wg_per_cu;
     const uint64_t lanes = (seg_bound + e->scan_info.chains - 1) / e->scan_info.chains;
     uint64_t block = (lanes + max_wgs - 1) / max_wgs;
-    block = std::min<uint64_t>(std::max<uint64_t>((block + 255) / 256 * 256, 256), e->scan_max_block);
+    block = std::min<uint64_t>(std::max<uint64_t>((block + 255) / 256 * 256, 256),
+                               std::min<uint64_t>(e->scan_max_block, (uint64_t)e->scan_info.threads));
     const uint64_t per_block = block * e->scan_info.chains;
     uint64_t grid = (seg_bound + per_block - 1) / per_block;
     grid = std::min<uint64_t>(grid, max_wgs);

@@ -25,6 +25,7 @@ struct ScanVariantInfo {
     int blk;         // bytes per lane per iteration (segment length must be a multiple)
     int fuse;        // cut walk in the epilogue when one wave = one buffer: 1 = from the bitmap
                      // (sweep only), 2 = from register candidate summaries (production)
+    int threads;     // widest workgroup the variant is compiled for
 };
 ScanVariantInfo scan_variant_info(int variant);
 

@@ -29,7 +29,8 @@ using ScanProd = ScanCfg<32, 1, false, 4, 16, 256, 2>;
 
 template <class CFG>
 constexpr ScanVariantInfo info_of() {
-    return {CFG::kCopies, CFG::kChains, CFG::kLds, CFG::kWavesPerSimd / 4, CFG::kBlk, CFG::kFuse};
+    return {CFG::kCopies, CFG::kChains, CFG::kLds, std::max(1, CFG::kWavesPerSimd * 256 / CFG::kThreads), CFG::kBlk,
+            CFG::kFuse, CFG::kThreads};
 }
 
 ScanVariantInfo scan_variant_info(int v) {
@@ -37,7 +38,7 @@ ScanVariantInfo scan_variant_info(int v) {
 #ifdef SDFS_TUNING
     return scan_variant_info_sweep(v);
 #else
-    return {0, 0, 0, 0, 0, 0};
+    return {0, 0, 0, 0, 0, 0, 0};
 #endif
 }
 

@@ -26,6 +26,12 @@ using ScanV9 = ScanCfg<32, 1, true, 4, 0, 128>;
 using ScanV10 = ScanCfg<32, 1, false, 4, 0, 256>;
 using ScanV15 = ScanCfg<32, 2, false, 4, 0, 256>;
 using ScanV19 = ScanCfg<32, 1, false, 4, 0, 128, 1>;  // 128-B blocks + bitmap-walk resolve in the epilogue
+// more independent rolling chains per SIMD at the same 128 KiB of tables: several segments per
+// lane, fewer waves, the register budget that frees (fused walk of every chain's buffer)
+using ScanV22 = ScanCfg<32, 2, false, 3, 16, 128, 2, 768>;  // 2 chains x 3 waves/SIMD, 168 VGPRs
+using ScanV26 = ScanCfg<32, 3, false, 2, 16, 128, 2, 512>;  // 3 chains x 2 waves/SIMD, 256 VGPRs
+using ScanV27 = ScanCfg<32, 4, false, 2, 16, 128, 2, 512>;  // 4 chains x 2 waves/SIMD
+using ScanV28 = ScanCfg<32, 2, false, 2, 16, 256, 2, 512>;  // 2 chains x 2 waves/SIMD, 256-B blocks
 // ablations (ids 11..25): 1 = no pop read, 2 = no push read, 4 = no candidate test, 8 = no
 // global loads; the skipped values are replaced by register values that keep the rest live
 using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;
@@ -37,7 +43,8 @@ using ScanA15 = ScanCfg<32, 1, false, 4, 15, 128>;
 
 template <class CFG>
 constexpr ScanVariantInfo sweep_info() {
-    return {CFG::kCopies, CFG::kChains, CFG::kLds, CFG::kWavesPerSimd / 4, CFG::kBlk, CFG::kFuse};
+    return {CFG::kCopies, CFG::kChains, CFG::kLds, std::max(1, CFG::kWavesPerSimd * 256 / CFG::kThreads), CFG::kBlk,
+            CFG::kFuse, CFG::kThreads};
 }
 
 ScanVariantInfo scan_variant_info_sweep(int v) {
@@ -64,7 +71,11 @@ ScanVariantInfo scan_variant_info_sweep(int v) {
     case 14: return sweep_info<ScanA4>();
     case 18: return sweep_info<ScanA8>();
     case 25: return sweep_info<ScanA15>();
-    default: return {0, 0, 0, 0, 0, 0};
+    case 22: return sweep_info<ScanV22>();
+    case 26: return sweep_info<ScanV26>();
+    case 27: return sweep_info<ScanV27>();
+    case 28: return sweep_info<ScanV28>();
+    default: return {0, 0, 0, 0, 0, 0, 0};
     }
 }
 
@@ -87,7 +98,8 @@ hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int var
     SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16)
     SWEEP_CASE(17, ScanV17) SWEEP_CASE(19, ScanV19) SWEEP_CASE(20, ScanV20) SWEEP_CASE(21, ScanV21)
     SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3) SWEEP_CASE(14, ScanA4)
-    SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15)
+    SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15) SWEEP_CASE(22, ScanV22) SWEEP_CASE(26, ScanV26)
+    SWEEP_CASE(27, ScanV27) SWEEP_CASE(28, ScanV28)
 #undef SWEEP_CASE
     default: return hipErrorInvalidValue;
     }
