@@ -529,3 +529,54 @@ def test_small_batch_latency_form_equals_throughput_form(algo):
         assert ss[b, :c].tolist() == es.tolist() and ls[b, :c].tolist() == el.tolist(), b
         assert (ds[b, :c, :dl] == ed).all(), b
     assert int(ls.max()) == prm["max_len"]  # a full maxLen chain went through the latency form
+
+
+def test_config2_8gib_half_duplicate_full_size():
+    """BASELINE configs[2] at its full size on one GPU: 8 GiB = 32768 write buffers of 256 KiB,
+    the second half byte copies of the first (50 % duplicate).  Copies give identical chunk lists
+    and digests; through the dedup-hit index every record of the second half is a duplicate whose
+    hashloc is its original's, every first-half record is new; a sample of buffers equals the
+    oracle (SparseDedupFile.java:435-446 drives the index this way)."""
+    from sdfs_amd.index import HipHashesMap
+
+    prm = P()
+    e = engine_for(prm)
+    half = 16384
+    batch = DeviceBatch(e, nbuf=2 * half, buf_len=262144)
+    batch.fill_streams(first_stream=0, bufs_per_stream=256)
+    v = batch.data.view(2 * half, 262144)
+    v[half:].copy_(v[:half])
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    _check_cover(counts, st, ln, 262144, prm)
+    assert (counts[half:] == counts[:half]).all()
+    assert (st[half:] == st[:half]).all() and (ln[half:] == ln[:half]).all() and (dg[half:] == dg[:half]).all()
+    _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 256, 0, [0, 5000, 16383])
+    n1 = int(counts[:half].sum())
+    ix = HipHashesMap(1 << 22)
+    dup, loc, _, new_count = ix.put_records(batch.record_table(), batch.total, pos_base=1)
+    torch.cuda.synchronize()
+    dup, loc = dup.cpu().numpy(), loc.cpu().numpy()
+    assert int(new_count.item()) == n1
+    assert (dup[:n1] == 0).all() and (dup[n1:total] == 1).all()
+    assert (loc[n1:total] == loc[:n1]).all()
+    ix.destroy()
+
+
+def test_config4_backup_per_gpu_share_16gib():
+    """BASELINE configs[4] (BACKUP_VOLUME, 128 GiB over 8 GPUs) at one GPU's share: 409 write
+    buffers of 40 MiB = 16 GiB, maxLen 128 KiB (VolumeConfigWriter.java:298-307), LDS-staged cut
+    walk.  Exact cover / min / max on every buffer; a sample equals the oracle."""
+    prm = P(max_len=131072)
+    e = engine_for(prm)
+    nbuf, L = 409, 40960 * 1024
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=L, records=False)
+    batch.fill_streams(first_stream=900, bufs_per_stream=1)
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    _check_cover(counts, st, ln, L, prm)
+    _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 1, 900, [0, 204, 408])
+    mean = nbuf * L / total
+    assert 7000 < mean < 9000, mean
