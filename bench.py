@@ -106,7 +106,7 @@ def git_head() -> str:
         return "unknown"
 
 
-class TwoStreamRunner:
+class StreamRunner:
     """Steps rotate over `depth` HIP streams on ONE engine (2 by default), each with its own output
     set (DeviceBatch) over the same resident input: `depth` batches in flight (the engine's
     workspace ring holds three)."""
@@ -250,7 +250,7 @@ def main():
     cs = torch.cuda.current_stream()
     base_id = rank * nbuf
     nsf = args.streams_in_flight
-    runner = TwoStreamRunner(torch, eng, batch, cs, DeviceBatch, nbuf, buf_len, device, depth=max(nsf, 2))
+    runner = StreamRunner(torch, eng, batch, cs, DeviceBatch, nbuf, buf_len, device, depth=max(nsf, 2))
     # N > 1: the one real exchange (all-gather of the fingerprint records), pipelined on a side
     # stream so step i's table travels while step i+1 is chunked (sdfs_amd/dist.py)
     ex = None
@@ -335,7 +335,7 @@ def main():
         e4 = HashFunctionPool(cfg4, device=local).getHashEngine()
         b4 = DeviceBatch(e4, nbuf=nbuf, buf_len=buf_len, device=device)
         b4.data = batch.data
-        r4 = TwoStreamRunner(torch, e4, b4, cs, DeviceBatch, nbuf, buf_len, device)
+        r4 = StreamRunner(torch, e4, b4, cs, DeviceBatch, nbuf, buf_len, device)
         for _ in range(3):
             r4.step(0)
         el = timed(torch, dist, 1, lambda: r4.step(0), args.steps)
