@@ -219,6 +219,9 @@ struct sdfs_cdc_engine {
     uint32_t scan_max_block = kScanThreads;  // widest scan workgroup (tuning build: SDFS_SCAN_MAX_BLOCK)
     bool hash_split = true;                  // latency form of the fingerprint for small batches (tuning: SDFS_HASH_SPLIT)
     bool small_seg = true;                   // short scan segments for small batches (tuning: SDFS_SMALL_SEG)
+    bool scan_prio = false;                  // pre-fingerprint stages on a high-priority stream (tuning: SDFS_SCAN_PRIO)
+    hipStream_t s_scan = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
@@ -379,6 +382,15 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
         if (e->run) e->runs_recorded++;
         return SDFS_CDC_OK;
     }
+    // Optional (tuning build: SDFS_SCAN_PRIO): the stages before the fingerprint run on a
+    // high-priority stream, so that with two batches in flight the dispatcher hands CUs freed by
+    // one batch's fingerprint kernel to the next batch's scan first.
+    const hipStream_t s_hash = s;
+    if (e->scan_prio && e->s_scan && nbuf >= (uint32_t)e->num_cus * 4) {
+        HIP_TRY(hipEventRecord(e->ev_fork, s_hash));
+        HIP_TRY(hipStreamWaitEvent(e->s_scan, e->ev_fork, 0));
+        s = e->s_scan;
+    }
     // A batch of fewer buffers than SIMDs (a coalescing-queue pass) scans in short segments: the
     // fused walk's one wave per buffer would leave most SIMDs idle and put a 4 KiB serial chain on
     // every lane (0.18 ms); 512-byte segments plus the separate walk take ~0.07 ms.
@@ -500,6 +512,11 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
         const int t = t_begin(e, K_SCATTER, s);
         HIP_TRY(launch_scatter(ca, s));
         t_end(e, t, s);
+    }
+    if (s != s_hash) {  // join: the fingerprint runs on the caller's stream
+        HIP_TRY(hipEventRecord(e->ev_join, s));
+        HIP_TRY(hipStreamWaitEvent(s_hash, e->ev_join, 0));
+        s = s_hash;
     }
     HashArgs ha{};
     ha.zero_page = e->zero_page.p;
@@ -1100,6 +1117,17 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_HASH_SPLIT")) e->hash_split = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SMALL_SEG")) e->small_seg = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SCAN_PRIO")) e->scan_prio = atoi(v) != 0;
+    if (e->scan_prio) {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&e->s_scan, hipStreamNonBlocking, hi) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
+            sdfs_cdc_destroy(e);
+            return fail(SDFS_CDC_EHIP, "scan-priority stream creation failed");
+        }
+    }
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif
@@ -1127,7 +1155,7 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
     {
         std::lock_guard<std::mutex> lk(e->mu);
         (void)hipSetDevice(e->prm.device);
-        for (hipStream_t s : {e->stream, e->s_h2d})
+        for (hipStream_t s : {e->stream, e->s_h2d, e->s_scan})
             if (s) (void)hipStreamSynchronize(s);
         for (hipStream_t s : e->qs)
             if (s) (void)hipStreamSynchronize(s);
@@ -1160,8 +1188,10 @@ int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
         for (auto& run : e->ev_runs)
             for (auto& ev : run.ev)
                 if (ev) (void)hipEventDestroy(ev);
-        for (hipStream_t s : {e->stream, e->s_h2d})
+        for (hipStream_t s : {e->stream, e->s_h2d, e->s_scan})
             if (s) (void)hipStreamDestroy(s);
+        for (hipEvent_t ev : {e->ev_fork, e->ev_join})
+            if (ev) (void)hipEventDestroy(ev);
         for (hipStream_t s : e->qs)
             if (s) (void)hipStreamDestroy(s);
     }
