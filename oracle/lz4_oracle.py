@@ -97,6 +97,37 @@ def compress_batch(base: np.ndarray, offs, lens, mode: int = R123, nthreads: int
     return [out[int(o): int(o) + int(n)].tobytes() for o, n in zip(out_offs, out_lens)], secs
 
 
+def system_batch(decompress: bool, base: np.ndarray, offs, lens, out_caps, nthreads: int = 16):
+    """The image's liblz4 (oracle/lz4_sys.c, dlopen'd) over many chunks on nthreads C threads:
+    LZ4_compress_default (out_caps = room per chunk) or LZ4_decompress_safe (out_caps = decoded
+    lengths).  Returns (out, out_offs, out_lens, seconds); the LZ4 bench's CPU legs only."""
+    import time
+
+    L = C.fast_lib()
+    if not getattr(L, "_lz4_sys_bound", False):
+        P = ctypes.POINTER
+        u8p, u32p, u64p = P(ctypes.c_uint8), P(ctypes.c_uint32), P(ctypes.c_uint64)
+        L.lz4_sys_batch.argtypes = [ctypes.c_int, u8p, u64p, u32p, ctypes.c_uint32, u8p, u64p, u32p, u32p, ctypes.c_int]
+        L.lz4_sys_batch.restype = ctypes.c_long
+        L._lz4_sys_bound = True
+    base = np.ascontiguousarray(base, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    caps = np.ascontiguousarray(out_caps, np.uint32)
+    out_offs = np.concatenate([[0], np.cumsum(caps.astype(np.uint64))[:-1]]).astype(np.uint64)
+    out = np.zeros(int(caps.astype(np.uint64).sum()) + 16, np.uint8)
+    out_lens = np.zeros(len(lens), np.uint32)
+    t0 = time.perf_counter()
+    rc = L.lz4_sys_batch(1 if decompress else 0, C._p(base, ctypes.c_uint8), C._p(offs, ctypes.c_uint64),
+                         C._p(lens, ctypes.c_uint32), len(lens), C._p(out, ctypes.c_uint8),
+                         C._p(out_offs, ctypes.c_uint64), C._p(caps, ctypes.c_uint32),
+                         C._p(out_lens, ctypes.c_uint32), nthreads)
+    secs = time.perf_counter() - t0
+    if rc != 0:
+        raise RuntimeError(f"lz4_sys_batch failed ({rc})")
+    return out, out_offs, out_lens, secs
+
+
 def decompress(block: bytes, n: int) -> bytes:
     a = _arr(block)
     out = np.zeros(max(n, 1), np.uint8)

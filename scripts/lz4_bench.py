@@ -60,6 +60,10 @@ def main():
     for ds in SETS:
         if ds == "random":
             batch.fill_streams(first_stream=0, bufs_per_stream=256)
+        elif ds == "mixed":  # every other buffer word salad: half the chunks compress, half do not
+            batch.fill_streams(first_stream=0, bufs_per_stream=256)
+            txt = torch.from_numpy(text_corpus((NBUF // 2) * L)).to(batch.data.device)
+            batch.data.view(NBUF, L)[1::2].copy_(txt.view(NBUF // 2, L))
         else:
             batch.data.copy_(torch.from_numpy(text_corpus(NBUF * L)).to(batch.data.device))
         batch.run()
@@ -124,6 +128,27 @@ def main():
                 break
             k = min(n, int(k * max(2.0, CPU_SECS / max(cpu_secs, 1e-3))))
         done_bytes = int(sl[sel].sum())
+        # the image's optimised liblz4 on the same sample (compress, then decode its own blocks)
+        sys_leg = None
+        if Z.system_lz4() is not None:
+            s_off, s_len = so[sel], sl[sel]
+            room = s_len + s_len // 255 + 16
+
+            def timed(fn):
+                tot, reps, r = 0.0, 0, None
+                while reps == 0 or tot < max(0.5, CPU_SECS / 4):
+                    r = fn()
+                    tot += r[3]
+                    reps += 1
+                return r, tot / reps
+
+            (cout, coffs, clens, _), ct = timed(lambda: Z.system_batch(False, host, s_off, s_len, room, THREADS))
+            (_, _, dlens, _), dt = timed(lambda: Z.system_batch(True, cout, coffs, clens, s_len, THREADS))
+            assert (dlens == s_len).all()
+            sys_leg = {"compress_gibps": round(done_bytes / ct / 2**30, 3),
+                       "decompress_gibps": round(done_bytes / dt / 2**30, 3), "threads": THREADS,
+                       "sample_chunks": int(k),
+                       "kind": "system liblz4 (LZ4_compress_default / LZ4_decompress_safe, V19 parse)"}
         print(json.dumps({
             "bench": "lz4_unique_chunks", "data": ds, "mode": mname, "chunks": int(n),
             "input_gib": round(nbytes / 2**30, 3), "kernel_ms": round(ms, 3),
@@ -131,6 +156,7 @@ def main():
             "decompress_ms": round(dms, 3), "decompress_gibps": round(nbytes / (dms / 1e3) / 2**30, 1),
             "cpu_baseline": {"gibps": round(done_bytes / cpu_secs / 2**30, 3), "threads": THREADS,
                              "sample_chunks": int(k), "kind": "port (oracle/lz4_ref.c)"},
+            "cpu_liblz4": sys_leg,
         }), flush=True)
 
 

@@ -2,12 +2,12 @@
 # PMC passes over the one-stream 4 GiB bench (BASELINE configs[1]): instruction mix and stall
 # counters of cdc_scan / chunk_hash, HBM traffic (FETCH_SIZE, WRITE_SIZE in separate passes:
 # gfx950 cannot collect both in one TCC pass).  Each pass is its own run under a time limit.
-# usage: scripts/pmc_scan.sh OUTDIR
+# usage: scripts/pmc_scan.sh OUTDIR   (PMC_CMD overrides the profiled command, e.g. the LZ4 bench)
 set -o pipefail
 OUT=${1:-gpurun_out/pmc}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-B="python3 bench.py --steps 6 --warmup 2 --threads= --at-4k 0 --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --compare 0 --streams-in-flight 1 --ramp-secs 0"
+B=${PMC_CMD:-"python3 bench.py --steps 6 --warmup 2 --threads= --at-4k 0 --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --compare 0 --streams-in-flight 1 --ramp-secs 0"}
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -- $B > "$OUT/$name.log" 2>&1

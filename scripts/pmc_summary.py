@@ -11,7 +11,8 @@ import json
 import os
 from collections import defaultdict
 
-KERNELS = {"cdc_scan_kernel": "cdc_scan", "chunk_hash_kernel": "chunk_hash"}
+KERNELS = {"cdc_scan_kernel": "cdc_scan", "chunk_hash_kernel": "chunk_hash", "lz4_lane_kernel": "lz4_lane",
+           "lz4_compress_kernel": "lz4_wave"}
 
 
 def collect(d):

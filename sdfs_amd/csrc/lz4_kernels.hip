@@ -49,7 +49,14 @@ struct Lz4Args {
     const uint64_t* dst_off;
     uint32_t* dst_len;
     uint32_t framed;
-    uint32_t* gtab;  // GTAB kernels: 16 KiB hash table per workgroup in global memory
+    uint32_t* gtab;  // GTAB kernels: 16 KiB hash table per workgroup in global memory;
+                     // LANE kernel: 2^13 tagged u32 entries per lane
+    uint32_t* ltag;  // LANE kernel: per-lane table generation
+    const uint32_t* idx;   // item i is chunk idx[i] (wave kernel: the lane pass's bailed chunks;
+                           // LANE kernel: chunks longest first)
+    uint32_t* bail;        // LANE kernel (hybrid): bail[0] = count, bail[1 + k] = chunk index
+    uint32_t bail_misses;  // LANE kernel (hybrid): hand a chunk to the wave pass after this many
+                           // consecutive search misses in its first quarter (0 = never)
 };
 
 // LDS byte scratch accessed as volatile LDS (ds_write_b8 / ds_read_u8, ordered per wave): a
@@ -84,6 +91,18 @@ __device__ __forceinline__ uint64_t ld64(lds_cu8* p) {
     lds_cu32* q = (lds_cu32*)(p - (a & 3));
     const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
     return (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, a & 3) << 32 | __builtin_amdgcn_alignbyte(w1, w0, a & 3);
+}
+
+// unaligned global words (one dword / dwordx2 load)
+__device__ __forceinline__ uint32_t g32(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+__device__ __forceinline__ uint64_t g64(const uint8_t* p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
 }
 
 // table index of the sequence at p (lz4_ref.c hash_at)
@@ -354,7 +373,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(Lz4Args a) {
     uint32_t* tab = GTAB ? a.gtab + (uint64_t)blockIdx.x * 4096 : ltab;
     const uint32_t lane = threadIdx.x;
     const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
-    for (uint64_t c = blockIdx.x; c < n_items; c += gridDim.x) {
+    for (uint64_t i = blockIdx.x; i < n_items; i += gridDim.x) {
+        const uint64_t c = a.idx ? a.idx[i] : i;
         const uint32_t n = a.src_len[c];
         const uint8_t* src = a.data + a.src_off[c];
         uint8_t* o = a.out + a.dst_off[c];
@@ -398,9 +418,25 @@ struct Lz4DecArgs {
     const uint32_t* dst_cap;
     uint32_t* dst_len;
     uint32_t framed;
+    uint32_t route;  // 0: every block; 1: compressible blocks only (lane kernel); 2: the others
 };
 
 constexpr uint32_t kLz4Corrupt = 0xFFFFFFFFu;
+
+// Routing of the split decode: a block that saved under 1/16 of its bytes (or a raw record) is
+// mostly literal runs, which the wave kernel copies coalesced; the others are short sequences,
+// which one lane per block parses without the wave's per-sequence round trips.
+__device__ __forceinline__ bool dec_lane_class(const uint8_t* in, uint32_t n, uint32_t cap, uint32_t framed) {
+    uint32_t out = cap;
+    if (framed) {
+        if (n < 4) return false;
+        const int32_t nz = (int32_t)((uint32_t)in[0] << 24 | (uint32_t)in[1] << 16 | (uint32_t)in[2] << 8 | in[3]);
+        if (nz <= 0) return false;
+        out = (uint32_t)nz;
+        n -= 4;
+    }
+    return (uint64_t)n * 16 < (uint64_t)out * 15;
+}
 
 // Decode one block of n bytes into dst (cap bytes); returns the decoded length or kLz4Corrupt.
 
@@ -485,6 +521,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(Lz4DecArgs a) {
         uint32_t n = a.src_len[c];
         uint8_t* o = a.out + a.dst_off[c];
         uint32_t cap = a.dst_cap[c];
+        if (a.route == 2 && dec_lane_class(in, n, cap, a.framed)) continue;  // the lane kernel's
         uint32_t got;
         if (a.framed) {  // [BE32 nz][payload]: nz > 0 = LZ4 block of nz bytes, else raw bytes
             if (n < 4) {
@@ -507,6 +544,82 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(Lz4DecArgs a) {
             got = decode_any<STAGE>(in, n, o, cap, stage, lane);
         }
         if (lane == 0) a.dst_len[c] = got;
+    }
+}
+
+// One LANE per block (route 1 of the split decode): the serial parse of decompress_block with
+// 8-byte literal and match copies (an overlapping match with offset < 8 byte by byte, which
+// reads only bytes this lane wrote before).  Same corruption checks, never writes past cap.
+__device__ uint32_t decompress_lane(const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ dst,
+                                    uint32_t cap) {
+    uint32_t ip = 0, op = 0;
+    for (;;) {
+        if (ip >= n) return kLz4Corrupt;
+        const uint32_t token = src[ip++];
+        uint32_t lit = token >> 4;
+        if (lit == kRunMask) {
+            uint32_t b;
+            do {
+                if (ip >= n) return kLz4Corrupt;
+                b = src[ip++];
+                lit += b;
+            } while (b == 255);
+        }
+        if (ip + lit > n || op + lit > cap) return kLz4Corrupt;
+        {
+            uint32_t k = 0;
+            for (; k + 8 <= lit; k += 8) {
+                const uint64_t v = g64(src + ip + k);
+                __builtin_memcpy(dst + op + k, &v, 8);
+            }
+            for (; k < lit; k++) dst[op + k] = src[ip + k];
+        }
+        ip += lit;
+        op += lit;
+        if (ip == n) return op;
+        if (ip + 2 > n) return kLz4Corrupt;
+        const uint32_t off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
+        ip += 2;
+        if (off == 0 || off > op) return kLz4Corrupt;
+        uint32_t ml = token & kMlMask;
+        if (ml == kMlMask) {
+            uint32_t b;
+            do {
+                if (ip >= n) return kLz4Corrupt;
+                b = src[ip++];
+                ml += b;
+            } while (b == 255);
+        }
+        ml += kMinMatch;
+        if (op + ml > cap) return kLz4Corrupt;
+        uint32_t k = 0;
+        if (off >= 8) {  // each 8-byte read ends at or before the first byte this step writes
+            for (; k + 8 <= ml; k += 8) {
+                const uint64_t v = g64(dst + op - off + k);
+                __builtin_memcpy(dst + op + k, &v, 8);
+            }
+        }
+        for (; k < ml; k++) dst[op + k] = dst[op - off + k];
+        op += ml;
+    }
+}
+
+__global__ __launch_bounds__(256) void lz4_decompress_lane_kernel(Lz4DecArgs a) {
+    const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
+    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < n_items; c += (uint64_t)gridDim.x * 256) {
+        const uint8_t* in = a.src + a.src_off[c];
+        uint32_t n = a.src_len[c];
+        const uint32_t cap = a.dst_cap[c];
+        if (!dec_lane_class(in, n, cap, a.framed)) continue;  // the wave kernel's
+        uint32_t got;
+        if (a.framed) {
+            const uint32_t nz = (uint32_t)in[0] << 24 | (uint32_t)in[1] << 16 | (uint32_t)in[2] << 8 | in[3];
+            got = nz <= cap ? decompress_lane(in + 4, n - 4, a.out + a.dst_off[c], nz) : kLz4Corrupt;
+            if (got != nz) got = kLz4Corrupt;
+        } else {
+            got = decompress_lane(in, n, a.out + a.dst_off[c], cap);
+        }
+        a.dst_len[c] = got;
     }
 }
 
@@ -605,6 +718,237 @@ __global__ __launch_bounds__(kPlanBlock) void lz4_plan_add_kernel(PlanArgs a) {
     if (i < n) a.dst_off[i] += a.bsum[blockIdx.x];
 }
 
+// ---- one LANE per chunk (measurement variant, SDFS_LZ4_LANE=1 in the tuning build): every
+// lane runs the byte-serial greedy parse of oracle/lz4_ref.c on its own chunk, so a wave has 64
+// chunks in flight instead of one; the lane's table is 2^13 u32 entries in global memory, each
+// (generation << 17) | position, so a new chunk starts from an "all zero" table without clearing
+// it (an entry of another generation reads as position 0, as LZ4's zeroed table does).
+constexpr uint32_t kLaneTabEntries = 1u << 13;
+constexpr uint32_t kLanePosBits = 17;  // positions < 128 KiB (the backup profile's maxLen)
+
+
+template <int MODE>
+__device__ __forceinline__ uint32_t lane_hash(const uint8_t* p, bool u16) {
+    if (u16) return (g32(p) * 2654435761u) >> 19;
+    if constexpr (MODE == SDFS_CDC_LZ4_V19) return (uint32_t)(((g64(p) << 24) * 889523592379ull) >> 52);
+    return (g32(p) * 2654435761u) >> 20;
+}
+
+__device__ __forceinline__ uint32_t lane_run(uint8_t* dst, uint32_t op, uint32_t len) {
+    for (; len >= 255; len -= 255) dst[op++] = 255;
+    dst[op++] = (uint8_t)len;
+    return op;
+}
+
+__device__ __forceinline__ void lane_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+    uint32_t k = 0;
+    for (; k + 4 <= n; k += 4) {
+        const uint32_t v = g32(src + k);
+        __builtin_memcpy(dst + k, &v, 4);
+    }
+    for (; k < n; k++) dst[k] = src[k];
+}
+
+constexpr uint32_t kLaneBailed = 0xffffffffu;
+constexpr uint32_t kHybridChunksPerCu = 192;  // auto policy: hybrid from 192 chunks per CU up
+constexpr int kLaneDepth = 1;  // probes per search round (SDFS_LZ4_LANE_DEPTH=4|8 in the tuning build:
+                               // no gain at 1 GiB batches, where table traffic, not the chain, bounds it)
+
+// The lane's search runs D probes per round: their positions follow from the step rule until a
+// match, so the D source words, then the D table entries, then the D candidate words are each
+// loaded together (three round trips per D probes instead of two or three per probe).  A probe
+// sees the puts of the earlier probes of its round by forwarding (same entry: the latest earlier
+// probe's position), exactly as the serial loop's get-after-put would.
+template <int MODE, int D>
+__device__ uint32_t compress_lane(const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ dst,
+                                  uint32_t* __restrict__ tab, uint32_t tag, uint32_t bail_misses) {
+    const bool u16 = n < kLimit64K;
+    const uint32_t mflimit = n >= kMfLimit ? n - kMfLimit : 0;
+    const uint32_t search_end = MODE == SDFS_CDC_LZ4_V19 ? mflimit + 1 : mflimit;
+    const uint32_t matchlimit = n >= kLastLiterals ? n - kLastLiterals : 0;
+    const uint32_t tg = tag << kLanePosBits;
+    auto get = [&](uint32_t h) -> uint32_t {
+        const uint32_t e = tab[h];
+        return (e & ~((1u << kLanePosBits) - 1)) == tg ? (e & ((1u << kLanePosBits) - 1)) : 0u;
+    };
+    auto put = [&](uint32_t h, uint32_t pos) { tab[h] = tg | pos; };
+    uint32_t ip = 0, anchor = 0, op = 0;
+    if (n >= kMfLimit + 1) {
+        put(lane_hash<MODE>(src, u16), 0);
+        ip = 1;
+        for (;;) {
+            uint32_t match = 0;
+            bool found = false;
+            {
+                uint32_t fip = ip, step = 1, nb = 1u << 6;
+                for (;;) {
+                    if (bail_misses && nb >= bail_misses + 64 && 4 * fip < n) return kLaneBailed;
+                    uint32_t pos[D], h[D], m[D], cur[D];
+                    int nv = 0;  // probes of this round the serial loop would make
+#pragma unroll
+                    for (int i = 0; i < D; i++) {
+                        pos[i] = fip;
+                        if (nv == i && fip + step <= search_end) nv = i + 1;
+                        fip += step;
+                        step = nb++ >> 6;
+                    }
+#pragma unroll
+                    for (int i = 0; i < D; i++) {
+                        cur[i] = i < nv ? g32(src + pos[i]) : 0u;
+                        h[i] = i < nv ? lane_hash<MODE>(src + pos[i], u16) : 0u;
+                    }
+#pragma unroll
+                    for (int i = 0; i < D; i++) m[i] = i < nv ? get(h[i]) : 0u;
+#pragma unroll
+                    for (int i = 1; i < D; i++)
+#pragma unroll
+                        for (int j = 0; j < i; j++)
+                            if (h[j] == h[i]) m[i] = pos[j];
+                    int hit = D;
+#pragma unroll
+                    for (int i = D - 1; i >= 0; i--) {
+                        const bool near = u16 || m[i] + kMaxDistance >= pos[i];
+                        if (i < nv && near && g32(src + m[i]) == cur[i]) hit = i;
+                    }
+                    const int last = hit < D ? hit : nv - 1;
+#pragma unroll
+                    for (int i = 0; i < D; i++)
+                        if (i <= last) put(h[i], pos[i]);
+                    if (hit < D) {
+#pragma unroll
+                        for (int i = 0; i < D; i++)
+                            if (i == hit) {
+                                ip = pos[i];
+                                match = m[i];
+                            }
+                        found = true;
+                        break;
+                    }
+                    if (nv < D) break;
+                }
+            }
+            if (!found) break;
+            while (ip > anchor && match > 0 && src[ip - 1] == src[match - 1]) {
+                ip--;
+                match--;
+            }
+            uint32_t token = op++;
+            {
+                const uint32_t lit = ip - anchor;
+                if (lit >= kRunMask) {
+                    dst[token] = (uint8_t)(kRunMask << 4);
+                    op = lane_run(dst, op, lit - kRunMask);
+                } else {
+                    dst[token] = (uint8_t)(lit << 4);
+                }
+                lane_copy(dst + op, src + anchor, lit);
+                op += lit;
+            }
+            bool done = false;
+            for (;;) {
+                const uint32_t off = ip - match;
+                dst[op++] = (uint8_t)off;
+                dst[op++] = (uint8_t)(off >> 8);
+                uint32_t a = ip + kMinMatch, b = match + kMinMatch;
+                // 32 bytes per round trip (four independent 8-byte pairs), then 8, then bytes
+                while (a + 32 <= matchlimit) {
+                    uint64_t x[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) x[k] = g64(src + a + 8 * k) ^ g64(src + b + 8 * k);
+                    int k = 0;
+                    while (k < 4 && x[k] == 0) k++;
+                    if (k < 4) {
+                        a += 8 * k + ((uint32_t)__builtin_ctzll(x[k]) >> 3);
+                        goto counted;
+                    }
+                    a += 32;
+                    b += 32;
+                }
+                while (a + 8 <= matchlimit) {
+                    const uint64_t x = g64(src + a) ^ g64(src + b);
+                    if (x) {
+                        a += (uint32_t)__builtin_ctzll(x) >> 3;
+                        goto counted;
+                    }
+                    a += 8;
+                    b += 8;
+                }
+                while (a < matchlimit && src[a] == src[b]) {
+                    a++;
+                    b++;
+                }
+            counted:
+                const uint32_t ml = a - (ip + kMinMatch);
+                ip = a;
+                if (ml >= kMlMask) {
+                    dst[token] += kMlMask;
+                    op = lane_run(dst, op, ml - kMlMask);
+                } else {
+                    dst[token] += (uint8_t)ml;
+                }
+                anchor = ip;
+                if (ip > mflimit) {
+                    done = true;
+                    break;
+                }
+                put(lane_hash<MODE>(src + ip - 2, u16), ip - 2);
+                const uint32_t h = lane_hash<MODE>(src + ip, u16);
+                match = get(h);
+                put(h, ip);
+                if ((u16 || match + kMaxDistance >= ip) && g32(src + match) == g32(src + ip)) {
+                    token = op++;
+                    dst[token] = 0;
+                    continue;
+                }
+                break;
+            }
+            if (done) break;
+            ++ip;
+        }
+    }
+    const uint32_t last = n - anchor;
+    if (last >= kRunMask) {
+        dst[op++] = (uint8_t)(kRunMask << 4);
+        op = lane_run(dst, op, last - kRunMask);
+    } else {
+        dst[op++] = (uint8_t)(last << 4);
+    }
+    lane_copy(dst + op, src + anchor, last);
+    return op + last;
+}
+
+template <int MODE, int D>
+__global__ __launch_bounds__(256) void lz4_lane_kernel(Lz4Args a) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nl = gridDim.x * 256;
+    const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
+    uint32_t* tab = a.gtab + (uint64_t)g * kLaneTabEntries;
+    uint32_t tag = a.ltag[g];
+    for (uint64_t i = g; i < n_items; i += nl) {
+        const uint64_t c = a.idx ? a.idx[i] : i;  // longest-first order: a wave's lanes end together
+        if (++tag >= (1u << (32 - kLanePosBits))) {  // generations exhausted: clear once
+            for (uint32_t i = 0; i < kLaneTabEntries; i++) tab[i] = 0;
+            tag = 1;
+        }
+        const uint32_t n = a.src_len[c];
+        uint8_t* o = a.out + a.dst_off[c];
+        const uint32_t hdr = a.framed ? 4u : 0u;
+        const uint32_t len = compress_lane<MODE, D>(a.data + a.src_off[c], n, o + hdr, tab, tag, a.bail_misses);
+        if (len == kLaneBailed) {
+            a.bail[1 + atomicAdd(a.bail, 1u)] = (uint32_t)c;
+            continue;
+        }
+        if (hdr) {
+            o[0] = (uint8_t)(n >> 24);
+            o[1] = (uint8_t)(n >> 16);
+            o[2] = (uint8_t)(n >> 8);
+            o[3] = (uint8_t)n;
+        }
+        a.dst_len[c] = len + hdr;
+    }
+    a.ltag[g] = tag;
+}
+
 template <typename T>
 struct ZBuf {
     T* p = nullptr;
@@ -637,8 +981,19 @@ struct sdfs_cdc_lz4 {
     int wg_per_cu = kLz4WgPerCu;  // SDFS_LZ4_WG_PER_CU overrides (measurements)
     int gtab_mode = 0;            // SDFS_LZ4_GTAB=1: hash tables in global memory
     int stage = 0;                // SDFS_LZ4_STAGE=16384|32768: chunks up to that size staged in LDS
+    int lane_mode = -1;           // -1 auto (hybrid from kHybridChunksPerCu chunks per CU up), 0 wave
+                                  // kernel, 1 lane kernel only, 2 hybrid (SDFS_LZ4_LANE, tuning build)
+    int lane_wg_per_cu = 4;       // SDFS_LZ4_LANE_WG_PER_CU: 256-thread workgroups per CU (lane mode)
+    ZBuf<uint32_t> ltag;
+    ZBuf<uint32_t> bail;          // hybrid (lane_mode 2): count + bailed chunk indices
+    uint32_t bail_misses = 128;   // SDFS_LZ4_BAIL
+    int lane_sort = 0;            // SDFS_LZ4_LANE_SORT=1: lanes take chunks longest first (measured slower)
+    int lane_depth = kLaneDepth;  // SDFS_LZ4_LANE_DEPTH
+    ZBuf<uint32_t> ord;           // launch_extent_order scratch: starts, tasks, total, hist, cursor
     int dec_stage = (int)kDecStage;
     int dec_wg_per_cu = kDecWgPerCu;
+    int dec_split = -1;  // -1 auto (split from kHybridChunksPerCu blocks per CU up), 0 wave kernel only,
+                         // 1 split: lanes for compressible blocks, waves for the rest (SDFS_LZ4_DEC_LANE)
     ZBuf<uint32_t> gtab;
     hipStream_t stream = nullptr;
     ZBuf<uint64_t> bsum;
@@ -659,8 +1014,85 @@ struct sdfs_cdc_lz4 {
 
 namespace {
 
+template <int D>
+hipError_t launch_lane_d(int mode, uint32_t grid, const Lz4Args& g, hipStream_t s) {
+    if (mode == SDFS_CDC_LZ4_V19)
+        hipLaunchKernelGGL((lz4_lane_kernel<SDFS_CDC_LZ4_V19, D>), dim3(grid), dim3(256), 0, s, g);
+    else
+        hipLaunchKernelGGL((lz4_lane_kernel<SDFS_CDC_LZ4_R123, D>), dim3(grid), dim3(256), 0, s, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_lane(int mode, int depth, uint32_t grid, const Lz4Args& g, hipStream_t s) {
+#ifdef SDFS_TUNING
+    if (depth == 4) return launch_lane_d<4>(mode, grid, g, s);
+    if (depth == 8) return launch_lane_d<8>(mode, grid, g, s);
+#endif
+    (void)depth;
+    return launch_lane_d<kLaneDepth>(mode, grid, g, s);
+}
+
+// Lane tables for `lanes` lanes (32 KiB each, zeroed once; generations make later chunks start
+// from an empty table).  False: not allocatable now (the wave kernel runs instead).
+bool lane_tables(sdfs_cdc_lz4* z, uint64_t lanes, hipStream_t s) {
+    if (z->ltag.n >= lanes && z->ltag.p) return true;
+    if (z->gtab.ensure(lanes * kLaneTabEntries) != hipSuccess || z->ltag.ensure(lanes) != hipSuccess) {
+        z->gtab.release();
+        z->ltag.release();
+        (void)hipGetLastError();
+        return false;
+    }
+    if (hipMemsetAsync(z->gtab.p, 0, lanes * kLaneTabEntries * 4, s) != hipSuccess ||
+        hipMemsetAsync(z->ltag.p, 0, lanes * 4, s) != hipSuccess) {
+        z->ltag.release();  // tables not known to be zero: allocate and clear again next time
+        return false;
+    }
+    return true;
+}
+
 int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
     if (a.n_max == 0) return SDFS_CDC_OK;
+    // Auto: a batch with enough chunks to fill the chip one lane per chunk runs the hybrid (lanes
+    // for compressible chunks, the wave kernel for the ones a lane bails on); smaller batches the
+    // wave kernel (scripts/lz4_batch_sweep.sh: the hybrid pays from ~50 000 chunks per 256 CUs).
+    // n_max bounds a device-count batch, so the choice follows the capacity the caller gives.
+    const int lane_mode = z->lane_mode >= 0 ? z->lane_mode
+                                            : (a.n_max >= (uint64_t)z->num_cus * kHybridChunksPerCu ? 2 : 0);
+    const uint64_t lgrid = std::min<uint64_t>((a.n_max + 255) / 256, (uint64_t)z->num_cus * z->lane_wg_per_cu);
+    if (lane_mode == 1 && !lane_tables(z, lgrid * 256, s))
+        return fail_status(SDFS_CDC_EHIP, "lz4: cannot allocate %llu lane tables", (unsigned long long)(lgrid * 256));
+    if (lane_mode == 1 || (lane_mode == 2 && lane_tables(z, lgrid * 256, s))) {
+        const uint64_t grid = lgrid;
+        Lz4Args g = a;
+        g.gtab = z->gtab.p;
+        g.ltag = z->ltag.p;
+        const bool hybrid = lane_mode == 2;
+        if (z->lane_sort) {
+            LZ_TRY(z->ord.ensure(2 * a.n_max + kExtentScratchWords));
+            ExtentArgs x{a.src_len, a.d_count, a.n_max, z->ord.p, z->ord.p + a.n_max, z->ord.p + 2 * a.n_max,
+                         z->ord.p + 2 * a.n_max + 1, z->ord.p + 2 * a.n_max + 1 + 512};
+            LZ_TRY(launch_extent_order(x, s));
+            g.idx = x.tasks;
+        }
+        if (hybrid) {
+            LZ_TRY(z->bail.ensure(a.n_max + 1));
+            LZ_TRY(hipMemsetAsync(z->bail.p, 0, 4, s));
+            g.bail = z->bail.p;
+            g.bail_misses = z->bail_misses;
+        }
+        LZ_TRY(launch_lane(z->mode, z->lane_depth, (uint32_t)grid, g, s));
+        if (!hybrid) return SDFS_CDC_OK;
+        Lz4Args w = a;  // the bailed chunks, one wave each
+        w.d_count = z->bail.p;
+        w.idx = z->bail.p + 1;
+        const uint32_t wgrid = (uint32_t)std::min<uint64_t>(a.n_max, (uint64_t)z->num_cus * z->wg_per_cu);
+        if (z->mode == SDFS_CDC_LZ4_V19)
+            hipLaunchKernelGGL(lz4_compress_kernel<SDFS_CDC_LZ4_V19>, dim3(wgrid), dim3(64), 0, s, w);
+        else
+            hipLaunchKernelGGL(lz4_compress_kernel<SDFS_CDC_LZ4_R123>, dim3(wgrid), dim3(64), 0, s, w);
+        LZ_TRY(hipGetLastError());
+        return SDFS_CDC_OK;
+    }
     const uint64_t grid = std::min<uint64_t>(a.n_max, (uint64_t)z->num_cus * z->wg_per_cu);
     if (z->gtab_mode) {
         LZ_TRY(z->gtab.ensure(grid * 4096));
@@ -722,7 +1154,13 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     if (z->stage) z->wg_per_cu = z->stage == 32768 ? 3 : 4;  // 16 KiB table + 1 KiB scratch + stage per workgroup
     if (const char* v = getenv("SDFS_LZ4_DEC_STAGE")) z->dec_stage = atoi(v) == 8192 ? 8192 : (int)kDecStage;
     if (const char* v = getenv("SDFS_LZ4_DEC_WG_PER_CU")) z->dec_wg_per_cu = std::max(1, atoi(v));
+    if (const char* v = getenv("SDFS_LZ4_DEC_LANE")) z->dec_split = atoi(v);
     if (const char* v = getenv("SDFS_LZ4_WG_PER_CU")) z->wg_per_cu = std::max(1, atoi(v));
+    if (const char* v = getenv("SDFS_LZ4_LANE")) z->lane_mode = atoi(v);
+    if (const char* v = getenv("SDFS_LZ4_LANE_WG_PER_CU")) z->lane_wg_per_cu = std::max(1, atoi(v));
+    if (const char* v = getenv("SDFS_LZ4_BAIL")) z->bail_misses = (uint32_t)std::max(0, atoi(v));
+    if (const char* v = getenv("SDFS_LZ4_LANE_SORT")) z->lane_sort = atoi(v);
+    if (const char* v = getenv("SDFS_LZ4_LANE_DEPTH")) z->lane_depth = atoi(v);
 #endif
     if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
         delete z;
@@ -740,6 +1178,9 @@ int sdfs_cdc_lz4_destroy(sdfs_cdc_lz4* z) {
         if (z->stream) (void)hipStreamSynchronize(z->stream);
         z->bsum.release();
         z->gtab.release();
+        z->ltag.release();
+        z->bail.release();
+        z->ord.release();
         z->h_in.release();
         z->h_out.release();
         z->h_soff.release();
@@ -856,6 +1297,15 @@ int sdfs_cdc_lz4_decompress_device(sdfs_cdc_lz4* z, const uint8_t* d_src, const 
     std::lock_guard<std::mutex> lk(z->mu);
     LZ_TRY(hipSetDevice(z->device));
     Lz4DecArgs a{d_src, d_src_off, d_src_len, d_count, n_max, d_out, d_dst_off, d_dst_cap, d_dst_len, framed ? 1u : 0u};
+    const bool split = z->dec_split >= 0 ? z->dec_split != 0 : n_max >= (uint64_t)z->num_cus * kHybridChunksPerCu;
+    if (split) {  // compressible blocks one lane each, then the rest one wave each (same stream)
+        a.route = 1;
+        const uint64_t lg = std::min<uint64_t>((n_max + 255) / 256, (uint64_t)z->num_cus * 8);
+        hipLaunchKernelGGL(lz4_decompress_lane_kernel, dim3((uint32_t)lg), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), a);
+        LZ_TRY(hipGetLastError());
+        a.route = 2;
+    }
     const uint64_t grid = std::min<uint64_t>(n_max, (uint64_t)z->num_cus * z->dec_wg_per_cu);
     if (z->dec_stage == 8192)
         hipLaunchKernelGGL(lz4_decompress_kernel<8192>, dim3((uint32_t)grid), dim3(64), 0,

@@ -45,6 +45,23 @@ needs_liblz4 = pytest.mark.skipif(Z.system_lz4() is None, reason="no system libl
 
 
 @needs_liblz4
+def test_liblz4_batch_baseline_matches_v19_and_round_trips():
+    """The LZ4 bench's liblz4 CPU leg (oracle/lz4_sys.c) makes the V19 oracle's blocks and
+    decodes them back."""
+    parts = [_gen(k, n, stream=60 + i) for i, (k, n) in enumerate((k, n) for k in KINDS for n in (0, 13, 5000, 70000))]
+    lens = np.array([len(p) for p in parts], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    base = np.frombuffer(b"".join(parts) + bytes(8), np.uint8)
+    out, oo, ol, _ = Z.system_batch(False, base, offs, lens, lens + lens // 255 + 16, 4)
+    for i, p in enumerate(parts):
+        assert out[int(oo[i]): int(oo[i]) + int(ol[i])].tobytes() == Z.compress(p, Z.V19), i
+    back, bo, bl, _ = Z.system_batch(True, out, oo, ol, lens, 4)
+    assert (bl == lens).all()
+    for i, p in enumerate(parts):
+        assert back[int(bo[i]): int(bo[i]) + len(p)].tobytes() == p, i
+
+
+@needs_liblz4
 @pytest.mark.parametrize("kind", KINDS)
 def test_oracle_v19_equals_system_liblz4(kind):
     for n in LENS:
@@ -230,11 +247,24 @@ def test_gpu_decompress_device_framed_records():
         d = _gen(kind, n, stream=300 + i)
         datas.append(d)
         recs.append(struct.pack(">i", -1) + d if i % 11 == 0 else Z.compress_framed(d))
+    # malformed records (decoded length -1): truncated block, nz larger than the block decodes
+    # to, a match offset reaching before the output start, a literal run past the block end,
+    # a zero offset, and a header-only record
+    good = Z.compress(_gen("text", 3000, 17))
+    bad = [struct.pack(">i", 3000) + good[:-7], struct.pack(">i", 3001) + good,
+           struct.pack(">i", 24) + bytes([0x40]) + b"abcd" + bytes([0x10, 0x00]) + bytes([0x50]) + b"abcde",
+           struct.pack(">i", 3000) + bytes([0xF0, 0x20]) + good[:30],
+           struct.pack(">i", 12) + bytes([0x40]) + b"abcd" + bytes([0x00, 0x00]) + bytes([0x40]) + b"wxyz",
+           b"\x00\x00"]
+    nbad = len(bad)
+    for i, r in enumerate(bad):
+        recs.append(r)
+        datas.append(None)
     src_off = np.concatenate([[0], np.cumsum([len(r) + 1 for r in recs[:-1]])]).astype(np.int64)
     base = np.zeros(int(src_off[-1]) + len(recs[-1]) + 16, np.uint8)
     for o, r in zip(src_off, recs):
         base[int(o): int(o) + len(r)] = np.frombuffer(r, np.uint8)
-    caps = np.array([len(d) for d in datas], np.int32)
+    caps = np.array([len(d) if d is not None else 4000 for d in datas], np.int32)
     dst_off = np.concatenate([[3], 3 + np.cumsum(caps[:-1].astype(np.int64) + 5)]).astype(np.int64)
     dev = torch.device("cuda:0")
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
@@ -246,4 +276,52 @@ def test_gpu_decompress_device_framed_records():
     torch.cuda.synchronize()
     o, dln = out.cpu().numpy(), dl.cpu().numpy()
     for i, d in enumerate(datas):
-        assert dln[i] == len(d) and o[dst_off[i]: dst_off[i] + len(d)].tobytes() == d, i
+        if d is None:
+            assert dln[i] == -1, i
+        else:
+            assert dln[i] == len(d) and o[dst_off[i]: dst_off[i] + len(d)].tobytes() == d, i
+    assert nbad == 6
+
+
+@pytest.mark.gpu
+def test_gpu_large_batch_hybrid_vs_oracle():
+    """A batch large enough for the product library's hybrid (one lane per chunk, bailed
+    incompressible chunks re-run one wave each: >= 192 chunks per CU): every record of a
+    half-random, half-text 512 MiB batch equals the oracle's, in both modes, and decodes back."""
+    torch = pytest.importorskip("torch")
+    from sdfs_amd import HipVariableSha256HashEngine
+    from sdfs_amd.device import DeviceBatch
+    e = HipVariableSha256HashEngine()
+    nbuf, L = 2048, 262144
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=L)
+    batch.fill_streams(first_stream=700, bufs_per_stream=64)
+    v = batch.data.view(nbuf, L)
+    src = Z.text_like(1, 77, 4 << 20)
+    txt = np.stack([src[(b * 12347) % (len(src) - L):][:L] for b in range(nbuf // 2)])
+    v[1::2].copy_(torch.from_numpy(txt).to(v.device))
+    v[6, 1000:90000] = 0  # long zero runs: 255-runs in the match lengths
+    batch.run()
+    recs = batch.record_table()
+    n = int(recs.shape[0])
+    assert n >= 192 * torch.cuda.get_device_properties(0).multi_processor_count
+    host = batch.data.cpu().numpy()
+    for mode in (Z.R123, Z.V19):
+        c = comp(mode)
+        src_off, src_len, dst_off, total = c.plan_records(recs, uniform_len=L)
+        out = torch.zeros(int(total.item()) + 16, dtype=torch.uint8, device="cuda")
+        dst_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+        c.compress_device(batch.data, src_off, src_len, out, dst_off, dst_len)
+        torch.cuda.synchronize()
+        so, sl, do, dl = (t.cpu().numpy() for t in (src_off, src_len, dst_off, dst_len))
+        ob = out.cpu().numpy()
+        want, _ = Z.compress_batch(host, so, sl, mode, 16)
+        bad = [i for i in range(n) if ob[int(do[i]): int(do[i]) + int(dl[i])].tobytes() != want[i]]
+        assert not bad, (len(bad), bad[:8])
+        # read side at the same size (the split decode: lanes for compressible records, waves
+        # for the rest): every record back to its chunk
+        back = torch.zeros_like(batch.data)
+        blen = torch.zeros(n, dtype=torch.int32, device="cuda")
+        c.decompress_device(out, dst_off, dst_len, back, src_off, src_len, blen)
+        torch.cuda.synchronize()
+        assert torch.equal(blen, src_len) and torch.equal(back, batch.data)
+    e.destroy()
