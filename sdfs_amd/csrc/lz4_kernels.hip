@@ -554,6 +554,54 @@ __device__ uint32_t decompress_lane(const uint8_t* __restrict__ src, uint32_t n,
                                     uint32_t cap) {
     uint32_t ip = 0, op = 0;
     for (;;) {
+        // fast sequence: short literal run (< 15) with its offset inside the next 17 source
+        // bytes and room for 16-byte literal / 8-byte-rounded match writes before cap.  The
+        // over-written bytes past op are rewritten by the following sequences before anything
+        // reads them (a match only reads below its own op).
+        if (ip + 17 <= n && op + 16 <= cap) {
+            const uint64_t w0 = g64(src + ip), l0 = g64(src + ip + 1), l1 = g64(src + ip + 9);
+            const uint32_t token = (uint32_t)w0 & 255u, lit = token >> 4;
+            if (lit < kRunMask) {
+                __builtin_memcpy(dst + op, &l0, 8);
+                __builtin_memcpy(dst + op + 8, &l1, 8);
+                // offset bytes at lit, lit + 1 of the 16 loaded after the token
+                const uint32_t b0 = lit < 8 ? (uint32_t)(l0 >> (8 * lit)) : (uint32_t)(l1 >> (8 * (lit - 8)));
+                const uint32_t b1 = lit + 1 < 8 ? (uint32_t)(l0 >> (8 * (lit + 1))) : (uint32_t)(l1 >> (8 * (lit - 7)));
+                const uint32_t off = (b0 & 255u) | ((b1 & 255u) << 8);
+                op += lit;
+                ip += 3 + lit;
+                if (off == 0 || off > op) return kLz4Corrupt;
+                uint32_t ml = token & kMlMask;
+                if (ml == kMlMask) {
+                    uint32_t b;
+                    do {
+                        if (ip >= n) return kLz4Corrupt;
+                        b = src[ip++];
+                        ml += b;
+                    } while (b == 255);
+                }
+                ml += kMinMatch;
+                if (op + ml > cap) return kLz4Corrupt;
+                uint32_t k = 0;
+                if (off >= 8) {
+                    if (op + ml + 8 <= cap) {  // 8-byte rounded (wild) copy
+                        for (; k < ml; k += 8) {
+                            const uint64_t v = g64(dst + op - off + k);
+                            __builtin_memcpy(dst + op + k, &v, 8);
+                        }
+                        k = ml;
+                    } else {
+                        for (; k + 8 <= ml; k += 8) {
+                            const uint64_t v = g64(dst + op - off + k);
+                            __builtin_memcpy(dst + op + k, &v, 8);
+                        }
+                    }
+                }
+                for (; k < ml; k++) dst[op + k] = dst[op - off + k];
+                op += ml;
+                continue;
+            }
+        }
         if (ip >= n) return kLz4Corrupt;
         const uint32_t token = src[ip++];
         uint32_t lit = token >> 4;
