@@ -965,8 +965,17 @@ __device__ uint32_t compress_lane(const uint8_t* __restrict__ src, uint32_t n, u
     return op + last;
 }
 
-template <int MODE, int D>
+// Hybrid pre-test (PT): before parsing, a lane looks at its chunk's first kPretestBytes for
+// repeated 4-byte sequences in a 64-entry table of its own in LDS (16-bit tags of the
+// multiplicative hash whose top 6 bits pick the entry; entry h of lane t at h * 256 + t).  Incompressible data repeats none (random
+// chunks: 0 hits; word-salad text: 21-66, scripts/lz4_bench.py data), so such a chunk goes
+// straight to the wave kernel instead of after 128 table-probing misses.  Only the route
+// depends on it; the bytes do not.
+constexpr uint32_t kPretestBytes = 512, kPretestHits = 4;
+
+template <int MODE, int D, bool PT>
 __global__ __launch_bounds__(256) void lz4_lane_kernel(Lz4Args a) {
+    __shared__ uint16_t pt[PT ? 64 * 256 : 1];  // 32 KiB: four 256-lane workgroups per CU
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nl = gridDim.x * 256;
     const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
@@ -974,14 +983,34 @@ __global__ __launch_bounds__(256) void lz4_lane_kernel(Lz4Args a) {
     uint32_t tag = a.ltag[g];
     for (uint64_t i = g; i < n_items; i += nl) {
         const uint64_t c = a.idx ? a.idx[i] : i;  // longest-first order: a wave's lanes end together
+        const uint32_t n = a.src_len[c];
+        const uint8_t* src = a.data + a.src_off[c];
+        if constexpr (PT) {
+            if (a.bail) {
+                const uint32_t m = n < kPretestBytes ? n : kPretestBytes;
+#pragma unroll 8
+                for (uint32_t h = 0; h < 64; h++) pt[h * 256 + threadIdx.x] = 0;
+                uint32_t hits = 0;
+#pragma unroll 4
+                for (uint32_t p = 0; p + 4 <= m; p++) {
+                    const uint32_t x = g32(src + p) * 2654435761u;  // slot: top 6 bits, tag: low 16
+                    const uint32_t h = x >> 26;
+                    hits += pt[h * 256 + threadIdx.x] == (uint16_t)x;
+                    pt[h * 256 + threadIdx.x] = (uint16_t)x;
+                }
+                if (hits < kPretestHits && m >= 64) {
+                    a.bail[1 + atomicAdd(a.bail, 1u)] = (uint32_t)c;
+                    continue;
+                }
+            }
+        }
         if (++tag >= (1u << (32 - kLanePosBits))) {  // generations exhausted: clear once
             for (uint32_t i = 0; i < kLaneTabEntries; i++) tab[i] = 0;
             tag = 1;
         }
-        const uint32_t n = a.src_len[c];
         uint8_t* o = a.out + a.dst_off[c];
         const uint32_t hdr = a.framed ? 4u : 0u;
-        const uint32_t len = compress_lane<MODE, D>(a.data + a.src_off[c], n, o + hdr, tab, tag, a.bail_misses);
+        const uint32_t len = compress_lane<MODE, D>(src, n, o + hdr, tab, tag, a.bail_misses);
         if (len == kLaneBailed) {
             a.bail[1 + atomicAdd(a.bail, 1u)] = (uint32_t)c;
             continue;
@@ -1037,6 +1066,7 @@ struct sdfs_cdc_lz4 {
     uint32_t bail_misses = 128;   // SDFS_LZ4_BAIL
     int lane_sort = 0;            // SDFS_LZ4_LANE_SORT=1: lanes take chunks longest first (measured slower)
     int lane_depth = kLaneDepth;  // SDFS_LZ4_LANE_DEPTH
+    int pretest = 1;              // SDFS_LZ4_PRETEST=0: no LDS pre-test in the hybrid (tuning build)
     ZBuf<uint32_t> ord;           // launch_extent_order scratch: starts, tasks, total, hist, cursor
     int dec_stage = (int)kDecStage;
     int dec_wg_per_cu = kDecWgPerCu;
@@ -1062,22 +1092,24 @@ struct sdfs_cdc_lz4 {
 
 namespace {
 
-template <int D>
+template <int D, bool PT>
 hipError_t launch_lane_d(int mode, uint32_t grid, const Lz4Args& g, hipStream_t s) {
     if (mode == SDFS_CDC_LZ4_V19)
-        hipLaunchKernelGGL((lz4_lane_kernel<SDFS_CDC_LZ4_V19, D>), dim3(grid), dim3(256), 0, s, g);
+        hipLaunchKernelGGL((lz4_lane_kernel<SDFS_CDC_LZ4_V19, D, PT>), dim3(grid), dim3(256), 0, s, g);
     else
-        hipLaunchKernelGGL((lz4_lane_kernel<SDFS_CDC_LZ4_R123, D>), dim3(grid), dim3(256), 0, s, g);
+        hipLaunchKernelGGL((lz4_lane_kernel<SDFS_CDC_LZ4_R123, D, PT>), dim3(grid), dim3(256), 0, s, g);
     return hipGetLastError();
 }
 
-hipError_t launch_lane(int mode, int depth, uint32_t grid, const Lz4Args& g, hipStream_t s) {
+hipError_t launch_lane(int mode, int depth, bool pretest, uint32_t grid, const Lz4Args& g, hipStream_t s) {
 #ifdef SDFS_TUNING
-    if (depth == 4) return launch_lane_d<4>(mode, grid, g, s);
-    if (depth == 8) return launch_lane_d<8>(mode, grid, g, s);
+    if (depth == 4) return launch_lane_d<4, false>(mode, grid, g, s);
+    if (depth == 8) return launch_lane_d<8, false>(mode, grid, g, s);
+    if (!pretest) return launch_lane_d<kLaneDepth, false>(mode, grid, g, s);
 #endif
     (void)depth;
-    return launch_lane_d<kLaneDepth>(mode, grid, g, s);
+    (void)pretest;
+    return launch_lane_d<kLaneDepth, true>(mode, grid, g, s);
 }
 
 // Lane tables for `lanes` lanes (32 KiB each, zeroed once; generations make later chunks start
@@ -1128,7 +1160,7 @@ int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
             g.bail = z->bail.p;
             g.bail_misses = z->bail_misses;
         }
-        LZ_TRY(launch_lane(z->mode, z->lane_depth, (uint32_t)grid, g, s));
+        LZ_TRY(launch_lane(z->mode, z->lane_depth, z->pretest != 0, (uint32_t)grid, g, s));
         if (!hybrid) return SDFS_CDC_OK;
         Lz4Args w = a;  // the bailed chunks, one wave each
         w.d_count = z->bail.p;
@@ -1209,6 +1241,7 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     if (const char* v = getenv("SDFS_LZ4_BAIL")) z->bail_misses = (uint32_t)std::max(0, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_LANE_SORT")) z->lane_sort = atoi(v);
     if (const char* v = getenv("SDFS_LZ4_LANE_DEPTH")) z->lane_depth = atoi(v);
+    if (const char* v = getenv("SDFS_LZ4_PRETEST")) z->pretest = atoi(v);
 #endif
     if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
         delete z;
