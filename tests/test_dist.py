@@ -1,4 +1,4 @@
-"""Multi-rank tests (gloo, world_size 2, CPU): stream sharding and the fingerprint-table all-gather
+"""Multi-rank tests (gloo, world_size 2, 3 and 8 (the driver's scaling run), CPU): stream sharding and the fingerprint-table all-gather
 that bench.py runs over RCCL at N>1 (sdfs_amd/dist.py)."""
 import os
 import socket
@@ -86,7 +86,7 @@ def _exchange_worker(rank, world, port, q, direct=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,direct", [(2, False), (3, False), (2, True), (3, True)])
+@pytest.mark.parametrize("world,direct", [(2, False), (3, False), (2, True), (3, True), (8, True)])
 def test_record_exchange_pipelined_gloo(world, direct):
     port = _free_port()
     ctx = mp.get_context("spawn")
@@ -145,8 +145,8 @@ def _shard_worker(rank, world, port, q):
         pool = torch.randint(0, 256, (40, 32), generator=g, dtype=torch.uint8)  # shared fingerprints
         rg = torch.Generator().manual_seed(100 + rank)
         picks = torch.randint(0, 40, (25 + 5 * rank,), generator=rg)
-        table = torch.zeros(40, RECORD_BYTES, dtype=torch.uint8)
         n = picks.shape[0]
+        table = torch.zeros(max(40, n), RECORD_BYTES, dtype=torch.uint8)
         table[:n, :32] = pool[picks]
         table[:n, 32] = rank
         table[:n, 33] = torch.arange(n, dtype=torch.uint8)
@@ -158,7 +158,7 @@ def _shard_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_dedup_index_gloo(world):
     port = _free_port()
     ctx = mp.get_context("spawn")
