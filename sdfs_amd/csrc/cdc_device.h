@@ -818,8 +818,20 @@ __device__ __forceinline__ void store_digest(const HashArgs& a, uint32_t slot, u
 // (wrong digests; every line is fetched once: the cost of the unaligned-line re-fetch).
 // Production ABL = 0.
 // BS = threads per workgroup; PF = load data block blk+1 while block blk is compressed.
+// ABL bit 32 (LDS-DMA prefetch): the next block goes straight to LDS (global_load_lds_dwordx4,
+// four per block: lane l's 16 bytes of quarter q land at q * 1024 + 16 l of its wave's 4 KiB),
+// so the prefetch holds no VGPRs (90 instead of 120: five waves per SIMD instead of four).
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+__device__ __forceinline__ void dma_block64(lds_u8* wave_lds, const uint8_t* q) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        __builtin_amdgcn_global_load_lds(q + 16 * j, (__attribute__((address_space(3))) void*)(wave_lds + 1024 * j), 16, 0,
+                                         0);
+}
+
 template <int ALGO, int ABL, bool PF>
-__device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
+__device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i, lds_u8* wave_lds = nullptr) {
     constexpr bool SHA = ALGO != 2;
     const uint32_t slot = a.tasks[i];
     const uint32_t b = slot / a.cap;
@@ -847,8 +859,12 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
     // load inside the branch, hipcc copied the new block into place before the compression and
     // so waited for it there (s_waitcnt vmcnt right after issuing: no prefetch at all).
     constexpr bool kPF2 = PF && (ABL & 16);
+    constexpr bool kDMA = PF && (ABL & 32);
+    const uint32_t lane = threadIdx.x & 63;
     uint4 nx[4];
-    if constexpr (kPF2) {
+    if constexpr (kDMA) {
+        dma_block64(wave_lds, nfull ? p : a.zero_page);
+    } else if constexpr (kPF2) {
         load_block64(nx, nfull ? p : a.zero_page);
     } else if constexpr (PF) {
         if (nfull) load_block64(nx, p);  // block 0 (a chunk shorter than 64 B has none to read)
@@ -856,14 +872,24 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
     for (uint32_t blk = 0; blk < nblocks; blk++) {
         uint32_t w[16];
         uint4 pf_cur[4];
-        if constexpr (kPF2) {
+        if constexpr (kDMA) {
+            __builtin_amdgcn_s_waitcnt(0);  // this block's DMA has landed
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(wave_lds + 1024 * q + 16 * lane);
+                pf_cur[q] = make_uint4(v.x, v.y, v.z, v.w);
+            }
+            __builtin_amdgcn_s_waitcnt(0);  // read out before the next DMA overwrites it
+            dma_block64(wave_lds, blk + 1 < nfull ? p + 64 * (blk + 1) : a.zero_page);
+        } else if constexpr (kPF2) {
 #pragma unroll
             for (int q = 0; q < 4; q++) pf_cur[q] = nx[q];
             load_block64(nx, blk + 1 < nfull ? p + 64 * (blk + 1) : a.zero_page);
         }
         if (blk < nfull) {
             uint4 cur[4];
-            if constexpr (kPF2) {
+            if constexpr (kPF2 || kDMA) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) cur[q] = pf_cur[q];
             } else if constexpr (PF) {
@@ -910,6 +936,7 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
             s[0] = m4[0]; s[1] = m4[1]; s[2] = m4[2]; s[3] = m4[3];
         }
     }
+    if constexpr (kDMA) __builtin_amdgcn_s_waitcnt(0);  // no DMA into LDS outlives the task
     store_digest<ALGO>(a, slot, b, k, cs, len, s);
 }
 
@@ -921,6 +948,7 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i) {
 template <int ALGO, int ABL = 0, int BS = 256, bool PF = false, bool PRIO = false, int WPE = 0>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1, 8)))
 void chunk_hash_kernel(HashArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t pf_lds[(ABL & 32) ? BS / 64 * 4096 : 16];
     const uint32_t i = blockIdx.x * BS + threadIdx.x;
     if (i >= *a.total) return;
     if constexpr (PRIO) {
@@ -932,7 +960,8 @@ void chunk_hash_kernel(HashArgs a) {
         else if (nb > 256)
             __builtin_amdgcn_s_setprio(1);
     }
-    hash_task<ALGO, ABL, PF>(a, i);
+    lds_u8* wave_lds = (lds_u8*)pf_lds + 4096 * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    hash_task<ALGO, ABL, PF>(a, i, (ABL & 32) ? wave_lds : nullptr);
 }
 
 // Persistent form: a fixed grid (a.persist_grid workgroups) whose waves take the next 64 tasks

@@ -138,6 +138,10 @@ hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant,
         if (!a.wave_ctr || !a.persist_grid) return hipErrorInvalidValue;
         hipLaunchKernelGGL((chunk_hash_persistent_kernel<0, true, 16>), dim3(a.persist_grid), dim3(256), 0, s, a);
         break;
+    // LDS-DMA prefetch (ABL bit 32): no VGPRs for the next block, five waves per SIMD
+    case 22: hipLaunchKernelGGL((chunk_hash_kernel<0, 48, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 23: hipLaunchKernelGGL((chunk_hash_kernel<0, 48, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 24: hipLaunchKernelGGL((chunk_hash_kernel<0, 48, 256, true, true, 6>), dim3(blocks), dim3(256), 0, s, a); break;
     // the prefetch before ABL bit 16 (its copy at the data/tail merge waited for the load)
     case 20: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
     default: return hipErrorInvalidValue;
