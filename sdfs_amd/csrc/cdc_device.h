@@ -948,7 +948,6 @@ __device__ __forceinline__ void hash_task(const HashArgs& a, uint32_t i, lds_u8*
 template <int ALGO, int ABL = 0, int BS = 256, bool PF = false, bool PRIO = false, int WPE = 0>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1, 8)))
 void chunk_hash_kernel(HashArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t pf_lds[(ABL & 32) ? BS / 64 * 4096 : 16];
     const uint32_t i = blockIdx.x * BS + threadIdx.x;
     if (i >= *a.total) return;
     if constexpr (PRIO) {
@@ -960,8 +959,12 @@ void chunk_hash_kernel(HashArgs a) {
         else if (nb > 256)
             __builtin_amdgcn_s_setprio(1);
     }
-    lds_u8* wave_lds = (lds_u8*)pf_lds + 4096 * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    hash_task<ALGO, ABL, PF>(a, i, (ABL & 32) ? wave_lds : nullptr);
+    lds_u8* wave_lds = nullptr;
+    if constexpr ((ABL & 32) != 0) {  // LDS only in the DMA-prefetch form
+        __shared__ __attribute__((aligned(16))) uint8_t pf_lds[BS / 64 * 4096];
+        wave_lds = (lds_u8*)pf_lds + 4096 * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    }
+    hash_task<ALGO, ABL, PF>(a, i, wave_lds);
 }
 
 // Persistent form: a fixed grid (a.persist_grid workgroups) whose waves take the next 64 tasks
