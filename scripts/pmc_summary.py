@@ -12,7 +12,8 @@ import os
 from collections import defaultdict
 
 KERNELS = {"cdc_scan_kernel": "cdc_scan", "chunk_hash_kernel": "chunk_hash", "lz4_lane_kernel": "lz4_lane",
-           "lz4_compress_kernel": "lz4_wave"}
+           "lz4_compress_kernel": "lz4_wave", "lz4_decompress_lane_kernel": "lz4_dec_lane",
+           "lz4_decompress_kernel": "lz4_dec_wave"}
 
 
 def collect(d):

@@ -1070,6 +1070,7 @@ struct sdfs_cdc_lz4 {
     ZBuf<uint32_t> ord;           // launch_extent_order scratch: starts, tasks, total, hist, cursor
     int dec_stage = (int)kDecStage;
     int dec_wg_per_cu = kDecWgPerCu;
+    int dec_lane_wg_per_cu = 8;  // SDFS_LZ4_DEC_LANE_WG_PER_CU: 256-lane workgroups per CU (split decode)
     int dec_split = -1;  // -1 auto (split from kHybridChunksPerCu blocks per CU up), 0 wave kernel only,
                          // 1 split: lanes for compressible blocks, waves for the rest (SDFS_LZ4_DEC_LANE)
     ZBuf<uint32_t> gtab;
@@ -1235,6 +1236,7 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     if (const char* v = getenv("SDFS_LZ4_DEC_STAGE")) z->dec_stage = atoi(v) == 8192 ? 8192 : (int)kDecStage;
     if (const char* v = getenv("SDFS_LZ4_DEC_WG_PER_CU")) z->dec_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_DEC_LANE")) z->dec_split = atoi(v);
+    if (const char* v = getenv("SDFS_LZ4_DEC_LANE_WG_PER_CU")) z->dec_lane_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_WG_PER_CU")) z->wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_LANE")) z->lane_mode = atoi(v);
     if (const char* v = getenv("SDFS_LZ4_LANE_WG_PER_CU")) z->lane_wg_per_cu = std::max(1, atoi(v));
@@ -1381,7 +1383,7 @@ int sdfs_cdc_lz4_decompress_device(sdfs_cdc_lz4* z, const uint8_t* d_src, const 
     const bool split = z->dec_split >= 0 ? z->dec_split != 0 : n_max >= (uint64_t)z->num_cus * kHybridChunksPerCu;
     if (split) {  // compressible blocks one lane each, then the rest one wave each (same stream)
         a.route = 1;
-        const uint64_t lg = std::min<uint64_t>((n_max + 255) / 256, (uint64_t)z->num_cus * 8);
+        const uint64_t lg = std::min<uint64_t>((n_max + 255) / 256, (uint64_t)z->num_cus * z->dec_lane_wg_per_cu);
         hipLaunchKernelGGL(lz4_decompress_lane_kernel, dim3((uint32_t)lg), dim3(256), 0,
                            reinterpret_cast<hipStream_t>(stream), a);
         LZ_TRY(hipGetLastError());
