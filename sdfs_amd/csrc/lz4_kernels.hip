@@ -1080,6 +1080,9 @@ struct sdfs_cdc_lz4 {
     ZBuf<uint8_t> h_in, h_out;
     ZBuf<uint64_t> h_soff, h_doff;
     ZBuf<uint32_t> h_slen, h_dlen;
+    hipEvent_t order_ev = nullptr;  // last launch that used the shared device scratch
+    hipStream_t order_stream = nullptr;
+    bool order_valid = false;
     std::mutex mu;
 };
 
@@ -1131,8 +1134,32 @@ bool lane_tables(sdfs_cdc_lz4* z, uint64_t lanes, hipStream_t s) {
     return true;
 }
 
+// The compressor's device scratch (lane tables and generations, the bail list, the plan's block
+// sums) serves one stream at a time: a launch on another stream than the previous one first
+// waits for that one's work (an event recorded after every launch that used the scratch).
+int scratch_acquire(sdfs_cdc_lz4* z, hipStream_t s) {
+    if (z->order_valid && z->order_stream != s) LZ_TRY(hipStreamWaitEvent(s, z->order_ev, 0));
+    return SDFS_CDC_OK;
+}
+int scratch_release(sdfs_cdc_lz4* z, hipStream_t s) {
+    LZ_TRY(hipEventRecord(z->order_ev, s));
+    z->order_valid = true;
+    z->order_stream = s;
+    return SDFS_CDC_OK;
+}
+
+int launch_compress_impl(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s);
+
 int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
     if (a.n_max == 0) return SDFS_CDC_OK;
+    int rc = scratch_acquire(z, s);
+    if (rc) return rc;
+    rc = launch_compress_impl(z, a, s);
+    const int rr = scratch_release(z, s);
+    return rc ? rc : rr;
+}
+
+int launch_compress_impl(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
     // Auto: a batch with enough chunks to fill the chip one lane per chunk runs the hybrid (lanes
     // for compressible chunks, the wave kernel for the ones a lane bails on); smaller batches the
     // wave kernel (scripts/lz4_batch_sweep.sh: the hybrid pays from ~50 000 chunks per 256 CUs).
@@ -1249,6 +1276,11 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
         delete z;
         return fail_status(SDFS_CDC_EHIP, "stream creation failed");
     }
+    if (hipEventCreateWithFlags(&z->order_ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(z->stream);
+        delete z;
+        return fail_status(SDFS_CDC_EHIP, "event creation failed");
+    }
     *out = z;
     return SDFS_CDC_OK;
 }
@@ -1271,6 +1303,7 @@ int sdfs_cdc_lz4_destroy(sdfs_cdc_lz4* z) {
         z->h_slen.release();
         z->h_dlen.release();
         if (z->stream) (void)hipStreamDestroy(z->stream);
+        if (z->order_ev) (void)hipEventDestroy(z->order_ev);
     }
     delete z;
     return SDFS_CDC_OK;
@@ -1307,13 +1340,14 @@ int sdfs_cdc_lz4_plan_records(sdfs_cdc_lz4* z, const uint8_t* d_records, const u
     }
     const uint32_t nblocks = (uint32_t)((n_max + kPlanBlock - 1) / kPlanBlock);
     LZ_TRY(z->bsum.ensure(nblocks));
+    if (int rc = scratch_acquire(z, s)) return rc;
     PlanArgs a{d_records, d_sel,     d_count,   n_max,     buffer_id_base, uniform_len,  framed ? 1u : 0u,
                d_buf_offs, d_src_off, d_src_len, d_dst_off, z->bsum.p,      d_total_bytes};
     hipLaunchKernelGGL(lz4_plan_local_kernel, dim3(nblocks), dim3(kPlanBlock), 0, s, a);
     hipLaunchKernelGGL(lz4_plan_scan_kernel, dim3(1), dim3(kPlanBlock), 0, s, z->bsum.p, nblocks, d_total_bytes);
     hipLaunchKernelGGL(lz4_plan_add_kernel, dim3(nblocks), dim3(kPlanBlock), 0, s, a);
     LZ_TRY(hipGetLastError());
-    return SDFS_CDC_OK;
+    return scratch_release(z, s);
 }
 
 int sdfs_cdc_lz4_compress_batch(sdfs_cdc_lz4* z, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,

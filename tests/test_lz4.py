@@ -317,6 +317,18 @@ def test_gpu_large_batch_hybrid_vs_oracle():
         want, _ = Z.compress_batch(host, so, sl, mode, 16)
         bad = [i for i in range(n) if ob[int(do[i]): int(do[i]) + int(dl[i])].tobytes() != want[i]]
         assert not bad, (len(bad), bad[:8])
+        # the same compressor from two streams at once (its lane tables and bail list are shared:
+        # the second launch must wait for the first): both outputs equal the checked one
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        outs = [torch.zeros_like(out) for _ in range(2)]
+        lens2 = [torch.zeros_like(dst_len) for _ in range(2)]
+        torch.cuda.synchronize()
+        for st_, o_, l_ in zip((s1, s2), outs, lens2):
+            with torch.cuda.stream(st_):
+                c.compress_device(batch.data, src_off, src_len, o_, dst_off, l_, stream=st_.cuda_stream)
+        torch.cuda.synchronize()
+        for o_, l_ in zip(outs, lens2):
+            assert torch.equal(l_, dst_len) and torch.equal(o_, out)
         # read side at the same size (the split decode: lanes for compressible records, waves
         # for the rest): every record back to its chunk
         back = torch.zeros_like(batch.data)
