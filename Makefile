@@ -12,7 +12,7 @@ TUNING_LIB := sdfs_amd/libsdfs_cdc_tuning.so
 SRCS := cdc_kernels cdc_engine dedup_index lz4_kernels map_emit aes_kernels
 OBJS := $(SRCS:%=build/%.o)
 TUNING_OBJS := $(SRCS:%=build/tuning/%.o) build/tuning/cdc_sweep.o
-HDRS := $(CSRC)/cdc_internal.h $(CSRC)/cdc_device.h $(CSRC)/host_queue.h $(wildcard include/*.h)
+HDRS := $(CSRC)/cdc_internal.h $(CSRC)/cdc_device.h $(CSRC)/host_queue.h $(CSRC)/stream_order.h $(wildcard include/*.h)
 
 all: $(LIB) tuning tools oracle
 

@@ -30,6 +30,7 @@
 
 #include "../../include/sdfs_aes.h"
 #include "cdc_internal.h"
+#include "stream_order.h"
 
 namespace sdfs {
 namespace {
@@ -599,6 +600,7 @@ struct sdfs_cdc_aes {
     ABuf<uint8_t> h_in, h_out;
     ABuf<uint64_t> h_soff, h_doff;
     ABuf<uint32_t> h_slen, h_dlen;
+    StreamOrder order;  // encryptions share plan/tasks: ordered across caller streams
     std::mutex mu;
 };
 
@@ -668,6 +670,7 @@ int encrypt_device(sdfs_cdc_aes* z, const uint8_t* d_src, const uint64_t* d_src_
     if (n_max >= (1ull << 32)) return fail_status(SDFS_CDC_EINVAL, "more than 2^32 records");
     AES_TRY(z->plan.ensure(2 * kAesBins));
     AES_TRY(z->tasks.ensure(n_max));
+    AES_TRY(z->order.acquire(s));
     AesPlanArgs pa{d_src_len, d_count, n_max, (uint32_t)plen, z->plan.p, z->plan.p + kAesBins, z->tasks.p};
     const uint32_t g = (uint32_t)((n_max + 255) / 256);
     AES_TRY(hipMemsetAsync(z->plan.p, 0, kAesBins * sizeof(uint32_t), s));
@@ -682,6 +685,7 @@ int encrypt_device(sdfs_cdc_aes* z, const uint8_t* d_src, const uint64_t* d_src_
     memcpy(a.rk, z->rk, sizeof(a.rk));
     launch_encrypt(z->nr, z->enc_variant, n_max, a, s);
     AES_TRY(hipGetLastError());
+    AES_TRY(z->order.release(s));
     return SDFS_CDC_OK;
 }
 
@@ -791,8 +795,9 @@ int sdfs_cdc_aes_create(int device, const uint8_t* key, uint32_t key_len, sdfs_c
     memcpy(img.data() + 512, t.isb, 1024);
     if (z->tabs.ensure(768) != hipSuccess ||
         hipMemcpy(z->tabs.p, img.data(), 768 * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess || z->order.init() != hipSuccess) {
         z->tabs.release();
+        if (z->stream) (void)hipStreamDestroy(z->stream);
         delete z;
         return fail_status(SDFS_CDC_EHIP, "AES table upload or stream creation failed");
     }
@@ -816,6 +821,7 @@ int sdfs_cdc_aes_destroy(sdfs_cdc_aes* z) {
         z->h_slen.release();
         z->h_dlen.release();
         if (z->stream) (void)hipStreamDestroy(z->stream);
+        z->order.destroy();
         memset(z->rk, 0, sizeof(z->rk));
         memset(z->dk, 0, sizeof(z->dk));
     }

@@ -33,6 +33,7 @@
 
 #include "../../include/sdfs_index.h"
 #include "cdc_internal.h"
+#include "stream_order.h"
 
 namespace sdfs {
 namespace {
@@ -305,6 +306,7 @@ struct sdfs_cdc_index {
     IxBuf<uint64_t> used;  // [1] device count of fingerprints held
     IxBuf<uint32_t> ltab, lcount, lslot, gidx, isnew, bsum, overflow;
     hipStream_t last = nullptr;
+    StreamOrder order;  // batches apply in call order whatever streams they come on
     std::mutex mu;
 };
 
@@ -328,6 +330,10 @@ int sdfs_cdc_index_create(int device, uint64_t capacity, sdfs_cdc_index** out) {
     IX_TRY(hipSetDevice(device));
     auto* ix = new sdfs_cdc_index();
     ix->device = device;
+    if (ix->order.init() != hipSuccess) {
+        delete ix;
+        return fail_status(SDFS_CDC_EHIP, "event creation failed");
+    }
     ix->slots = next_pow2(capacity + capacity / 7 + 1);
     ix->max_fill = ix->slots - ix->slots / 8;
     if (ix->table.ensure(ix->slots) != hipSuccess || ix->used.ensure(1) != hipSuccess ||
@@ -354,6 +360,7 @@ int sdfs_cdc_index_destroy(sdfs_cdc_index* ix) {
     ix->used.release();
     for (auto* b : {&ix->ltab, &ix->lcount, &ix->lslot, &ix->gidx, &ix->isnew, &ix->bsum, &ix->overflow})
         b->release();
+    ix->order.destroy();
     delete ix;
     return SDFS_CDC_OK;
 }
@@ -382,9 +389,11 @@ int sdfs_cdc_index_put_records(sdfs_cdc_index* ix, const uint8_t* d_records, uin
                                (unsigned long long)used, (unsigned long long)ix->max_fill,
                                (unsigned long long)n_max);
     }
+    IX_TRY(ix->order.acquire(s));
     ix->last = s;
     if (n_max == 0) {
         IX_TRY(hipMemsetAsync(d_new_count, 0, sizeof(uint64_t), s));
+        IX_TRY(ix->order.release(s));
         return SDFS_CDC_OK;
     }
     const uint64_t lsize = std::max<uint64_t>(64, next_pow2(2 * n_max));
@@ -413,6 +422,7 @@ int sdfs_cdc_index_put_records(sdfs_cdc_index* ix, const uint8_t* d_records, uin
     hipLaunchKernelGGL(ix_output_kernel, dim3(g), dim3(kIxThreads), 0, s, d_count, n_max, ix->isnew.p, ix->lslot.p,
                        ix->gidx.p, ix->table.p, d_dup, d_hashloc);
     IX_TRY(hipGetLastError());
+    IX_TRY(ix->order.release(s));
     ix->used_ub += n_max;
     return SDFS_CDC_OK;
 }
@@ -425,11 +435,13 @@ int sdfs_cdc_index_get(sdfs_cdc_index* ix, const uint8_t* d_digests, uint64_t n,
     std::lock_guard<std::mutex> lk(ix->mu);
     IX_TRY(hipSetDevice(ix->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    IX_TRY(ix->order.acquire(s));
     ix->last = s;
     const uint64_t g = (n + kIxThreads - 1) / kIxThreads;
     hipLaunchKernelGGL(ix_get_kernel, dim3((uint32_t)g), dim3(kIxThreads), 0, s, d_digests, n, ix->table.p,
                        ix->slots - 1, d_pos, d_refcount);
     IX_TRY(hipGetLastError());
+    IX_TRY(ix->order.release(s));
     return SDFS_CDC_OK;
 }
 
@@ -438,9 +450,11 @@ int sdfs_cdc_index_clear(sdfs_cdc_index* ix, void* stream) {
     std::lock_guard<std::mutex> lk(ix->mu);
     IX_TRY(hipSetDevice(ix->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    IX_TRY(ix->order.acquire(s));
     IX_TRY(hipMemsetAsync(ix->table.p, 0, ix->slots * sizeof(IndexSlot), s));
     IX_TRY(hipMemsetAsync(ix->used.p, 0, sizeof(uint64_t), s));
     IX_TRY(hipMemsetAsync(ix->overflow.p, 0, sizeof(uint32_t), s));
+    IX_TRY(ix->order.release(s));
     ix->used_ub = 0;
     ix->last = s;
     return SDFS_CDC_OK;

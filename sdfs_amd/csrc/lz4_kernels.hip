@@ -28,6 +28,7 @@
 
 #include "../../include/sdfs_lz4.h"
 #include "cdc_internal.h"
+#include "stream_order.h"
 
 namespace sdfs {
 namespace {
@@ -1080,9 +1081,7 @@ struct sdfs_cdc_lz4 {
     ZBuf<uint8_t> h_in, h_out;
     ZBuf<uint64_t> h_soff, h_doff;
     ZBuf<uint32_t> h_slen, h_dlen;
-    hipEvent_t order_ev = nullptr;  // last launch that used the shared device scratch
-    hipStream_t order_stream = nullptr;
-    bool order_valid = false;
+    StreamOrder order;  // launches that use the shared device scratch, across streams
     std::mutex mu;
 };
 
@@ -1138,13 +1137,11 @@ bool lane_tables(sdfs_cdc_lz4* z, uint64_t lanes, hipStream_t s) {
 // sums) serves one stream at a time: a launch on another stream than the previous one first
 // waits for that one's work (an event recorded after every launch that used the scratch).
 int scratch_acquire(sdfs_cdc_lz4* z, hipStream_t s) {
-    if (z->order_valid && z->order_stream != s) LZ_TRY(hipStreamWaitEvent(s, z->order_ev, 0));
+    LZ_TRY(z->order.acquire(s));
     return SDFS_CDC_OK;
 }
 int scratch_release(sdfs_cdc_lz4* z, hipStream_t s) {
-    LZ_TRY(hipEventRecord(z->order_ev, s));
-    z->order_valid = true;
-    z->order_stream = s;
+    LZ_TRY(z->order.release(s));
     return SDFS_CDC_OK;
 }
 
@@ -1276,7 +1273,7 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
         delete z;
         return fail_status(SDFS_CDC_EHIP, "stream creation failed");
     }
-    if (hipEventCreateWithFlags(&z->order_ev, hipEventDisableTiming) != hipSuccess) {
+    if (z->order.init() != hipSuccess) {
         (void)hipStreamDestroy(z->stream);
         delete z;
         return fail_status(SDFS_CDC_EHIP, "event creation failed");
@@ -1303,7 +1300,7 @@ int sdfs_cdc_lz4_destroy(sdfs_cdc_lz4* z) {
         z->h_slen.release();
         z->h_dlen.release();
         if (z->stream) (void)hipStreamDestroy(z->stream);
-        if (z->order_ev) (void)hipEventDestroy(z->order_ev);
+        z->order.destroy();
     }
     delete z;
     return SDFS_CDC_OK;

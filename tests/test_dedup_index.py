@@ -144,6 +144,30 @@ def test_index_random_batches_vs_oracle():
 
 
 @pytest.mark.gpu
+def test_index_batches_from_two_streams_apply_in_call_order():
+    """Batches enqueued back to back on different streams (flush threads with their own
+    streams) apply in call order: the second sees every fingerprint the first inserted."""
+    torch = pytest.importorskip("torch")
+    from sdfs_amd.index import HipHashesMap
+    rng = random.Random(21)
+    ix = HipHashesMap(1 << 18)
+    digests, bids = _random_batch(rng, 6000, 20, [], 0.0)
+    rec = torch.from_numpy(_records(digests, bids)).cuda()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        d1, l1, _, n1 = ix.put_records(rec, None, 0, stream=s1.cuda_stream)
+    with torch.cuda.stream(s2):
+        d2, l2, _, n2 = ix.put_records(rec, None, 1 << 30, stream=s2.cuda_stream)
+    torch.cuda.synchronize()
+    m = D.HashesMap()
+    edup, eloc, _ = D.write_buffers(m, [d.ljust(32, b"\0") for d in digests], bids, 0)
+    assert d1.cpu().tolist() == edup and l1.cpu().tolist() == eloc
+    assert int(n2.item()) == 0 and all(d2.cpu().tolist()) and l2.cpu().tolist() == l1.cpu().tolist()
+    ix.destroy()
+
+
+@pytest.mark.gpu
 def test_index_device_count_and_empty_batch():
     torch = pytest.importorskip("torch")
     from sdfs_amd.index import HipHashesMap
