@@ -13,6 +13,7 @@
  * These entry points encrypt a whole batch of records on the GPU, byte-identical to that cipher
  * (oracle/aes_ref.c restates FIPS-197 + SP 800-38A CBC + PKCS#5; tests pin it against FIPS/NIST
  * vectors and the image's openssl).  Errors, threading and sdfs_cdc_last_error() as in sdfs_cdc.h.
+ * Encryptions enqueued on different streams are ordered (they share the cipher's scheduling scratch).
  */
 #ifndef SDFS_AES_H
 #define SDFS_AES_H

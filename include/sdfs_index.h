@@ -21,6 +21,8 @@
  * HashBlobArchive does for the reference.
  *
  * Errors, threading and the last-error message follow include/sdfs_cdc.h (sdfs_cdc_last_error).
+ * Calls apply in call order whatever streams they are enqueued on (a call on another stream than
+ * the previous one waits for it on the device).
  * A full index returns SDFS_CDC_ECAP (HashtableFullException in the reference).
  */
 #ifndef SDFS_INDEX_H

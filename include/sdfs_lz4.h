@@ -14,6 +14,8 @@
  * greedy LZ4 parse (oracle/lz4_ref.c restates it; mode SDFS_CDC_LZ4_V19 is pinned there against
  * the image's liblz4 1.9.x, mode SDFS_CDC_LZ4_R123 is the reference's r123 rules).  The framed
  * form writes the putChunk record.  Errors, threading and sdfs_cdc_last_error() as in sdfs_cdc.h.
+ * Device-path calls may come on different streams: launches that share the compressor's device
+ * scratch wait for the previous such launch when it was enqueued on another stream.
  */
 #ifndef SDFS_LZ4_H
 #define SDFS_LZ4_H
