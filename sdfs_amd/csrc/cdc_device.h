@@ -36,9 +36,32 @@ __device__ __forceinline__ uint32_t bitop3_and_or(uint32_t a, uint32_t b, uint32
 // test, 8 = no global loads.  The skipped values are replaced by register values that keep every
 // remaining instruction live.  Bit 16 is not an ablation but a code layout (production): whole
 // blocks are loaded and scanned in a branch of their own (see the scan kernel's block loop).
+//
+// Mirrored state (ABL bit kAblMirror, ScanCfg MIRROR): the same recurrence on R = bitrev64(fp),
+// held as hi:lo = R >> 32 : R.  fp << 8 becomes R >> 8, the incoming byte lands bit-reversed in
+// R's top byte, and fp bits 0..31 (the predicate's field) are hi bits 31..0 — so a low-k-bit
+// zero predicate is ONE compare (hi < 2^(32-k)) instead of v_and + v_cmp.  The data dwords are
+// bit-reversed once after their load (byte p of a dword becomes byte 3-p, bits reversed), the
+// push index rev8(j) sits at lo bits [64-d, 72-d) (jshift = 64 - d), and the LDS tables hold
+// bitrev64(push[rev8(x)]) / bitrev64(pop[rev8(x)]) at entry x (build_table_image, mirror).
+constexpr int kAblMirror = 64;
+
 template <int P, int Q, int ABL = 0>
 __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
                                           uint32_t push_base, uint32_t jshift, const uint8_t* tab) {
+    if constexpr ((ABL & kAblMirror) != 0) {
+        const uint32_t pa = bitop3_and_or(lo >> (jshift - 8), 0xFF00u, push_base);
+        // (rev8(o) << 8) | c8; a byte already at bits 8..15 needs only the full-rate v_bitop3
+        const uint32_t qa = Q == 2 ? bitop3_and_or(odw, 0xFF00u, c8)
+                                   : __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + 3 - Q) << 8));
+        const uint2 pv = *reinterpret_cast<const uint2*>(tab + pa);
+        const uint2 qv = *reinterpret_cast<const uint2*>(tab + qa);
+        const uint32_t nlo = __builtin_amdgcn_alignbit(hi, lo, 8);                      // R >> 8, low word
+        const uint32_t nhi = __builtin_amdgcn_perm(hi, dw, 0x00070605u | ((3u - P) << 24));  // (hi >> 8) | rev8(b) << 24
+        lo = xor3(nlo, pv.x, qv.x);
+        hi = xor3(nhi, pv.y, qv.y);
+        return;
+    }
     // push[j] address (j << 8) | push_base with j = (fp >> (d-8)) & 0xFF = hi bits [jshift, jshift+8):
     // one full-rate shift + one v_bitop3 ((A & B) | C, table 0xEA) instead of v_bfe + v_lshl_or
     // (both half-rate on gfx950, scripts/isa_microbench.hip).
@@ -53,9 +76,17 @@ __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t d
 }
 
 // push-only step (window warm-up from the zero state; no byte leaves the window yet)
-template <int P>
+template <int P, bool M = false>
 __device__ __forceinline__ void push_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t push_base,
                                           uint32_t jshift, const uint8_t* tab) {
+    if constexpr (M) {
+        const uint2 pv = *reinterpret_cast<const uint2*>(tab + bitop3_and_or(lo >> (jshift - 8), 0xFF00u, push_base));
+        const uint32_t nlo = __builtin_amdgcn_alignbit(hi, lo, 8);
+        const uint32_t nhi = __builtin_amdgcn_perm(hi, dw, 0x00070605u | ((3u - P) << 24));
+        lo = nlo ^ pv.x;
+        hi = nhi ^ pv.y;
+        return;
+    }
     const uint2 pv = *reinterpret_cast<const uint2*>(tab + bitop3_and_or(hi >> (jshift - 8), 0xFF00u, push_base));
     const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);
     const uint32_t nlo = __builtin_amdgcn_perm(lo, dw, 0x06050400u | P);
@@ -67,11 +98,19 @@ __device__ __forceinline__ void push_step(uint32_t& lo, uint32_t& hi, uint32_t d
 // bit-reversed once per 32 positions).  Written as one v_and/v_cmp/v_addc sequence: in plain C
 // hipcc reassociates the 32 per-byte tests of a word into an OR tree at the end of the word,
 // keeping all 32 fingerprints live (scratch spills on every byte).
-template <bool PRED64>
+// Predicate kinds PK: 0 = (lo & mask) == val on one word, 1 = both words, 2 (mirrored state
+// only) = the low k fp bits all zero, i.e. `lo` (here the mirrored hi word) < a.thr = 2^(32-k).
+// `lo` is the word holding fp bits 0..31 (mirrored: R's hi word, masks bit-reversed by the host).
+template <int PK>
 __device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t hi, const ScanArgs& a) {
-    uint32_t t;
-    if constexpr (PRED64) {
-        uint32_t t2;
+    if constexpr (PK == 2) {
+        asm("v_cmp_gt_u32 vcc, %2, %1\n\t"
+            "v_addc_co_u32 %0, vcc, %0, %0, vcc"
+            : "+v"(bits)
+            : "v"(lo), "s"(a.thr)
+            : "vcc");
+    } else if constexpr (PK == 1) {
+        uint32_t t, t2;
         asm("v_and_b32 %1, %4, %3\n\t"
             "v_xor_b32 %1, %5, %1\n\t"
             "v_and_b32 %2, %7, %6\n\t"
@@ -83,6 +122,7 @@ __device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t
             : "v"(lo), "s"(a.mask_lo), "s"(a.val_lo), "v"(hi), "s"(a.mask_hi), "s"(a.val_hi)
             : "vcc");
     } else {
+        uint32_t t;
         asm("v_and_b32 %1, %3, %2\n\t"
             "v_cmp_eq_u32 vcc, %4, %1\n\t"
             "v_addc_co_u32 %0, vcc, %0, %0, vcc"
@@ -94,7 +134,7 @@ __device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t
 
 // Byte O of the current block (BLKW dwords), with the byte that leaves the window at O - W: in
 // this block when O >= W, otherwise in `prev` (the previous block's last 64 bytes).
-template <int W, bool PRED64, int O, int ABL, int BLKW>
+template <int W, int PK, int O, int ABL, int BLKW>
 __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& bits, const uint32_t (&cur)[BLKW],
                                           const uint32_t (&prev)[16], uint32_t c8, uint32_t push_base,
                                           const uint8_t* tab, const ScanArgs& a) {
@@ -104,8 +144,10 @@ __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& 
     roll_step<(O & 3), (OI & 3), ABL>(lo, hi, cur[O >> 2], odw, c8, push_base, a.jshift, tab);
     if constexpr (ABL & 4)
         bits ^= lo;
+    else if constexpr ((ABL & kAblMirror) != 0)
+        cand_shift<PK>(bits, hi, lo, a);
     else
-        cand_shift<PRED64>(bits, lo, hi, a);
+        cand_shift<PK>(bits, lo, hi, a);
 }
 
 // Byte O of every chain at once (NCH > 1): all chains' lookup addresses and their 2 x NCH LDS
@@ -113,7 +155,7 @@ __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& 
 // waitcnt pass then waits lgkmcnt(2 x later chains) before each chain's update).  The reads are
 // volatile so that they stay in issue order ahead of the updates: left alone, hipcc reuses one
 // destination pair for every chain and waits lgkmcnt(0) per chain.
-template <int W, bool PRED64, int O, int NCH, int BLKW>
+template <int W, int PK, int O, int NCH, int BLKW>
 __device__ __forceinline__ void bytes_multi(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
                                             const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
                                             uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
@@ -139,7 +181,7 @@ __device__ __forceinline__ void bytes_multi(uint32_t (&lo)[NCH], uint32_t (&hi)[
         const uint32_t nlo = __builtin_amdgcn_perm(lo[c], cur[c][O >> 2], 0x06050400u | (O & 3));
         lo[c] = xor3(nlo, pv[c].x, qv[c].x);
         hi[c] = xor3(nhi, pv[c].y, qv[c].y);
-        cand_shift<PRED64>(bits[c], lo[c], hi[c], a);
+        cand_shift<PK>(bits[c], lo[c], hi[c], a);
     }
 }
 
@@ -150,33 +192,33 @@ constexpr int kSchedGroup = SDFS_SCAN_SCHED_GROUP;  // bytes per scheduling regi
 
 // Positions O .. O0+31 of one candidate word, all chains interleaved (independent rolling chains
 // give the ILP that hides the LDS latency of the push lookups).
-template <int W, bool PRED64, int O0, int O, int NCH, int ABL, int BLKW>
+template <int W, int PK, int O0, int O, int NCH, int ABL, int BLKW>
 __device__ __forceinline__ void word_steps(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
                                            const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
                                            uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
     if constexpr (O < O0 + 32) {
         if constexpr (NCH > 1 && ABL == 0) {
-            bytes_multi<W, PRED64, O, NCH, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+            bytes_multi<W, PK, O, NCH, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
         } else {
 #pragma unroll
             for (int c = 0; c < NCH; c++)
-                byte_step<W, PRED64, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
+                byte_step<W, PK, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
         }
         if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) {
             // keep the scheduler from hoisting every (chain-independent) pop read of the block
             // ahead of the rolling chain: that costs ~2 VGPRs per byte and spills.
             __builtin_amdgcn_sched_barrier(0);
         }
-        word_steps<W, PRED64, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+        word_steps<W, PK, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
     }
 }
 
-template <int W, int O>
+template <int W, int O, bool M = false>
 __device__ __forceinline__ void warm_from(uint32_t& lo, uint32_t& hi, const uint32_t (&prev)[16], uint32_t push_base,
                                           uint32_t jshift, const uint8_t* tab) {
     if constexpr (O < 64) {
-        push_step<(O & 3)>(lo, hi, prev[O >> 2], push_base, jshift, tab);
-        warm_from<W, O + 1>(lo, hi, prev, push_base, jshift, tab);
+        push_step<(O & 3), M>(lo, hi, prev[O >> 2], push_base, jshift, tab);
+        warm_from<W, O + 1, M>(lo, hi, prev, push_base, jshift, tab);
     }
 }
 
@@ -200,18 +242,27 @@ __device__ __forceinline__ void load_block(uint32_t (&d)[N], const uint8_t* data
 }
 
 // All candidate words of one block: word WI covers positions 32*WI .. 32*WI+31.
-template <int W, bool PRED64, int WI, int NW, int NCH, int ABL, int BLKW>
+// Mirrored state: each word's 8 data dwords are bit-reversed in place right before its first
+// position (not at the load: hipcc then hoists all 64 reversals above the first byte and waits for
+// every load of the block there, and keeps raw and reversed copies live).
+template <int W, int PK, int WI, int NW, int NCH, int ABL, int BLKW>
 __device__ __forceinline__ void block_words(uint32_t (&words)[NCH][NW], uint32_t (&lo)[NCH], uint32_t (&hi)[NCH],
-                                            const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
+                                            uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
                                             uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
     if constexpr (WI < NW) {
+        if constexpr ((ABL & kAblMirror) != 0) {
+#pragma unroll
+            for (int c = 0; c < NCH; c++)
+#pragma unroll
+                for (int i = 8 * WI; i < 8 * WI + 8; i++) cur[c][i] = __builtin_bitreverse32(cur[c][i]);
+        }
         uint32_t bits[NCH];
 #pragma unroll
         for (int c = 0; c < NCH; c++) bits[c] = 0;
-        word_steps<W, PRED64, 32 * WI, 32 * WI, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+        word_steps<W, PK, 32 * WI, 32 * WI, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
 #pragma unroll
         for (int c = 0; c < NCH; c++) words[c][WI] = __builtin_bitreverse32(bits[c]);
-        block_words<W, PRED64, WI + 1, NW, NCH, ABL, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+        block_words<W, PK, WI + 1, NW, NCH, ABL, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
     }
 }
 
@@ -437,8 +488,10 @@ __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint3
 // THREADS and WPS: 512 / waves-per-SIMD VGPRs, so 768 threads at 3 waves/SIMD allow 168).
 // With FUSE 2 and two chains, chain c of a wave covers segments base + c * blockDim.x + 64w ..
 // + 63, i.e. its own buffer, and the epilogue walks both buffers.
-template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64, int FUSE = 0, int THREADS = kScanThreads>
+template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64, int FUSE = 0, int THREADS = kScanThreads,
+          bool MIRROR = false>
 struct ScanCfg {
+    static constexpr bool kMirror = MIRROR;  // bit-reversed rolling state (roll_step, kAblMirror)
     static constexpr int kFuse = NCH == 1 ? FUSE : (FUSE == 2 ? 2 : 0);  // resolve each wave's buffer(s) in the epilogue
     static constexpr int kThreads = THREADS;
     static constexpr int kAbl = ABL;
@@ -451,8 +504,11 @@ struct ScanCfg {
     static constexpr int kBlk = BLK;
 };
 
-template <int W, bool PRED64, class CFG>
+template <int W, int PK, class CFG>
 __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
+    static_assert(!CFG::kMirror || (CFG::kChains == 1 && !CFG::kPrefetch), "mirrored state: one chain, no prefetch");
+    static_assert(CFG::kMirror || PK != 2, "the one-compare predicate needs the mirrored state");
+    constexpr int MB = CFG::kMirror ? kAblMirror : 0;
     constexpr int NCH = CFG::kChains;
     constexpr int C = CFG::kCopies;
     constexpr int BLK = CFG::kBlk;
@@ -535,12 +591,15 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
         for (int c = 0; c < NCH; c++) {
             if (nblk[c] != 0 && !first[c]) {
                 load_block<16>(prev[c], a.data, start[c] - 64, start[c]);
+                if constexpr (CFG::kMirror)
+#pragma unroll
+                    for (int i = 0; i < 16; i++) prev[c][i] = __builtin_bitreverse32(prev[c][i]);
             } else {
 #pragma unroll
                 for (int i = 0; i < 16; i++) prev[c][i] = 0;  // bytes before the buffer are empty
             }
             lo[c] = hi[c] = 0;
-            warm_from<W, 64 - W>(lo[c], hi[c], prev[c], push_base, a.jshift, tab);
+            warm_from<W, 64 - W, CFG::kMirror>(lo[c], hi[c], prev[c], push_base, a.jshift, tab);
             if constexpr (CFG::kPrefetch) {
                 const bool act = nblk[c] != 0;
                 cur_full[c] = load_block_nb<BLKW>(cur[c], a.data, a.zero_page, act ? start[c] : 0, act ? end[c] : 0);
@@ -572,7 +631,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
                             cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
                         }
                     }
-                    block_words<W, PRED64, 0, BLK / 32, NCH, 0, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+                    block_words<W, PK, 0, BLK / 32, NCH, MB, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
                 }
             }
             if (!split_fast) {
@@ -591,7 +650,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
                     load_block<BLKW>(cur[c], a.data, act ? start[c] + (uint64_t)BLK * blk : 0, act ? end[c] : 0);
                 }
             }
-            block_words<W, PRED64, 0, BLK / 32, NCH, CFG::kAbl & 15, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+            block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 15) | MB, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
             }
             if constexpr (CFG::kFuse == 2) {
                 // candidates are rare (~1 per 4 KiB): a divergent, seldom-taken append

@@ -67,9 +67,18 @@ uint64_t mulx_mod(uint64_t v, uint64_t poly, int d) {
     return v;
 }
 
+uint64_t bitrev64_host(uint64_t v) {
+    uint64_t r = 0;
+    for (int i = 0; i < 64; i++) r |= ((v >> i) & 1) << (63 - i);
+    return r;
+}
+uint32_t bitrev32_host(uint32_t v) { return (uint32_t)(bitrev64_host(v) >> 32); }
+uint32_t rev8_host(uint32_t v) { return (uint32_t)(bitrev64_host(v) >> 56); }
+
 // Rolling-hash tables (same definition as the jar's precompute), laid out as the
-// scan kernel's LDS image with `copies` lane-private copies (cdc_internal.h).
-std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window, int copies) {
+// scan kernel's LDS image with `copies` lane-private copies (cdc_internal.h).  `mirror`: the
+// tables of the bit-reversed state (cdc_device.h roll_step): entry x = bitrev64(table[rev8(x)]).
+std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window, int copies, bool mirror) {
     const int d = poly_degree(poly);
     std::vector<uint64_t> push(256), pop(256);
     for (uint64_t i = 0; i < 256; i++) {
@@ -79,6 +88,15 @@ std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window, int copie
         uint64_t q = i;
         for (uint32_t k = 0; k < 8 * window; k++) q = mulx_mod(q, poly, d);
         pop[i] = q;
+    }
+    if (mirror) {
+        std::vector<uint64_t> mpush(256), mpop(256);
+        for (uint32_t x = 0; x < 256; x++) {
+            mpush[x] = bitrev64_host(push[rev8_host(x)]);
+            mpop[x] = bitrev64_host(pop[rev8_host(x)]);
+        }
+        push.swap(mpush);
+        pop.swap(mpop);
     }
     std::vector<uint8_t> img(scan_lds_bytes(copies));
     const uint32_t push_off = copies == 32 ? 0x10000u : 0x80u;
@@ -409,6 +427,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
         t_end(e, t, s);
     }
     const bool pred64 = (e->prm.pred_mask >> 32) != 0;
+    int pk = pred64 ? 1 : 0;
     ScanArgs sa{};
     sa.data = d_data;
     sa.offs = d_offs;
@@ -417,11 +436,26 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     sa.nbuf = nbuf;
     sa.uniform_len = uniform_len;
     sa.seg_len = seg_len;
-    sa.jshift = (uint32_t)(e->degree - 40);
-    sa.mask_lo = (uint32_t)e->prm.pred_mask;
-    sa.mask_hi = (uint32_t)(e->prm.pred_mask >> 32);
-    sa.val_lo = (uint32_t)e->prm.pred_value;
-    sa.val_hi = (uint32_t)(e->prm.pred_value >> 32);
+    if (e->scan_info.mirror) {
+        // bit-reversed state: fp bits 0..31 are the reversed hi word (cdc_device.h roll_step)
+        const uint64_t m = e->prm.pred_mask, v = e->prm.pred_value;
+        sa.jshift = (uint32_t)(64 - e->degree);
+        sa.mask_lo = bitrev32_host((uint32_t)m);
+        sa.mask_hi = bitrev32_host((uint32_t)(m >> 32));
+        sa.val_lo = bitrev32_host((uint32_t)v);
+        sa.val_hi = bitrev32_host((uint32_t)(v >> 32));
+        if (!pred64 && m != 0 && (m & (m + 1)) == 0 && v == 0) {  // low k bits zero: one compare
+            const int k = __builtin_popcountll(m);
+            sa.thr = k == 32 ? 1u : 1u << (32 - k);
+            pk = 2;
+        }
+    } else {
+        sa.jshift = (uint32_t)(e->degree - 40);
+        sa.mask_lo = (uint32_t)e->prm.pred_mask;
+        sa.mask_hi = (uint32_t)(e->prm.pred_mask >> 32);
+        sa.val_lo = (uint32_t)e->prm.pred_value;
+        sa.val_hi = (uint32_t)(e->prm.pred_value >> 32);
+    }
     sa.tab_image = e->tab_image.p;
     sa.zero_page = e->zero_page.p;
     uint64_t seg_bound;
@@ -477,7 +511,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
     grid = std::max<uint64_t>(grid, 1);
     {
         const int t = t_begin(e, K_SCAN, s);
-        HIP_TRY(launch_scan(sa, (int)e->prm.window, pred64, e->scan_variant, (int)grid, (int)block, s));
+        HIP_TRY(launch_scan(sa, (int)e->prm.window, pk, e->scan_variant, (int)grid, (int)block, s));
         t_end(e, t, s);
     }
     if (!fused) {
@@ -1136,7 +1170,7 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
         sdfs_cdc_destroy(e);
         return fail(SDFS_CDC_EINVAL, "bad scan variant/segment length");
     }
-    std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies);
+    std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies, e->scan_info.mirror != 0);
     if (e->zero_page.ensure(256) != hipSuccess || hipMemset(e->zero_page.p, 0, 256) != hipSuccess ||
         e->tab_image.ensure(img.size()) != hipSuccess ||
         hipMemcpy(e->tab_image.p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {

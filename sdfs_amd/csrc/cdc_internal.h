@@ -26,6 +26,7 @@ struct ScanVariantInfo {
     int fuse;        // cut walk in the epilogue when one wave = one buffer: 1 = from the bitmap
                      // (sweep only), 2 = from register candidate summaries (production)
     int threads;     // widest workgroup the variant is compiled for
+    int mirror;      // bit-reversed rolling state (mirrored LDS tables, one-compare predicate)
 };
 ScanVariantInfo scan_variant_info(int variant);
 
@@ -70,8 +71,10 @@ struct ScanArgs {
     uint32_t nbuf;
     uint32_t uniform_len;        // != 0 -> uniform layout
     uint32_t seg_len;            // bytes per segment, multiple of 64
-    uint32_t jshift;             // deg(P) - 40 : bit offset of the push index inside the hi word
-    uint32_t mask_lo, mask_hi, val_lo, val_hi;
+    uint32_t jshift;             // bit offset of the push index in the word holding it: deg(P) - 40
+                                 // (hi word), mirrored 64 - deg(P) (lo word of bitrev64(fp))
+    uint32_t mask_lo, mask_hi, val_lo, val_hi;  // mirrored: bit-reversed, lo = the word of fp bits 0..31
+    uint32_t thr;                // predicate kind 2: 2^(32-k) for a zero test of the low k fp bits
     const uint8_t* tab_image;    // global copy of the LDS image (scan_lds_bytes(copies))
     const uint8_t* zero_page;    // 256 zero bytes (branch-free prefetch of tail blocks)
     // fused cut resolution: when every wave's 64 segments are exactly one buffer (uniform layout,
@@ -153,7 +156,9 @@ inline uint64_t splitmix64_host(uint64_t x) {
 // kernel launchers (cdc_kernels.hip); all asynchronous on `stream`
 hipError_t launch_seg_prefix(const uint32_t* lens, uint32_t nbuf, uint32_t seg_len, uint64_t* seg_prefix,
                              hipStream_t stream);
-hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, int block,
+// pk: predicate kind (cand_shift): 0 = one 32-bit word, 1 = both words, 2 = low-k zero (mirrored
+// variants only)
+hipError_t launch_scan(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
                        hipStream_t stream);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
@@ -169,7 +174,7 @@ bool scan_window_supported(int window);
 #ifdef SDFS_TUNING
 // measurement-only variants (cdc_sweep.hip; tuning library only)
 ScanVariantInfo scan_variant_info_sweep(int variant);
-hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int variant, int grid, int block,
+hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
                              hipStream_t stream);
 hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);
 #endif

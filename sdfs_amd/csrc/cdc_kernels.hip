@@ -24,13 +24,16 @@ namespace sdfs {
 // one 1024-thread workgroup per CU), one 4 KiB segment per lane, 256-byte blocks (two whole
 // 128-byte lines per lane per iteration, so no line is fetched twice), the split fast-path
 // body (ABL bit 16) and the cut walk fused into the epilogue from register summaries (FUSE 2).
-// Interleaved A/B on MI355X against the alternatives is in DESIGN.md §7-8.
-using ScanProd = ScanCfg<32, 1, false, 4, 16, 256, 2>;
+// Bit-reversed (mirrored) rolling state (cdc_device.h roll_step): a low-k-bit zero predicate is
+// one compare, 9.4 instead of 10.1 VALU per byte.
+// Interleaved A/B on MI355X against the alternatives is in DESIGN.md §7-8 (sweep variant 29 =
+// this configuration with the plain state).
+using ScanProd = ScanCfg<32, 1, false, 4, 16, 256, 2, kScanThreads, true>;
 
 template <class CFG>
 constexpr ScanVariantInfo info_of() {
     return {CFG::kCopies, CFG::kChains, CFG::kLds, std::max(1, CFG::kWavesPerSimd * 256 / CFG::kThreads), CFG::kBlk,
-            CFG::kFuse, CFG::kThreads};
+            CFG::kFuse, CFG::kThreads, CFG::kMirror};
 }
 
 ScanVariantInfo scan_variant_info(int v) {
@@ -47,27 +50,29 @@ bool scan_window_supported(int window) {
 }
 
 template <int W, class CFG>
-static hipError_t launch_scan_wc(const ScanArgs& a, bool pred64, int grid, int block, hipStream_t s) {
-    if (pred64)
-        hipLaunchKernelGGL((cdc_scan_kernel<W, true, CFG>), dim3(grid), dim3(block), 0, s, a);
+static hipError_t launch_scan_wc(const ScanArgs& a, int pk, int grid, int block, hipStream_t s) {
+    if (pk == 1)
+        hipLaunchKernelGGL((cdc_scan_kernel<W, 1, CFG>), dim3(grid), dim3(block), 0, s, a);
+    else if (pk == 2 && CFG::kMirror)
+        hipLaunchKernelGGL((cdc_scan_kernel<W, CFG::kMirror ? 2 : 0, CFG>), dim3(grid), dim3(block), 0, s, a);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<W, false, CFG>), dim3(grid), dim3(block), 0, s, a);
+        hipLaunchKernelGGL((cdc_scan_kernel<W, 0, CFG>), dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const ScanArgs& a, int window, bool pred64, int variant, int grid, int block, hipStream_t s) {
+hipError_t launch_scan(const ScanArgs& a, int window, int pk, int variant, int grid, int block, hipStream_t s) {
     if (variant != 0) {
 #ifdef SDFS_TUNING
-        return launch_scan_sweep(a, window, pred64, variant, grid, block, s);
+        return launch_scan_sweep(a, window, pk, variant, grid, block, s);
 #else
         return hipErrorInvalidValue;
 #endif
     }
     switch (window) {
-    case 16: return launch_scan_wc<16, ScanProd>(a, pred64, grid, block, s);
-    case 32: return launch_scan_wc<32, ScanProd>(a, pred64, grid, block, s);
-    case 48: return launch_scan_wc<48, ScanProd>(a, pred64, grid, block, s);
-    case 64: return launch_scan_wc<64, ScanProd>(a, pred64, grid, block, s);
+    case 16: return launch_scan_wc<16, ScanProd>(a, pk, grid, block, s);
+    case 32: return launch_scan_wc<32, ScanProd>(a, pk, grid, block, s);
+    case 48: return launch_scan_wc<48, ScanProd>(a, pk, grid, block, s);
+    case 64: return launch_scan_wc<64, ScanProd>(a, pk, grid, block, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -34,6 +34,9 @@ using ScanV27 = ScanCfg<32, 4, false, 2, 16, 128, 2, 512>;  // 4 chains x 2 wave
 using ScanV28 = ScanCfg<32, 2, false, 2, 16, 256, 2, 512>;  // 2 chains x 2 waves/SIMD, 256-B blocks
 // ablations (ids 11..25): 1 = no pop read, 2 = no push read, 4 = no candidate test, 8 = no
 // global loads; the skipped values are replaced by register values that keep the rest live
+// production before / with the bit-reversed (mirrored) rolling state
+using ScanV29 = ScanCfg<32, 1, false, 4, 16, 256, 2>;
+using ScanV30 = ScanCfg<32, 1, false, 4, 16, 256, 2, kScanThreads, true>;
 using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;
 using ScanA2 = ScanCfg<32, 1, false, 4, 2, 128>;
 using ScanA3 = ScanCfg<32, 1, false, 4, 3, 128>;
@@ -44,7 +47,7 @@ using ScanA15 = ScanCfg<32, 1, false, 4, 15, 128>;
 template <class CFG>
 constexpr ScanVariantInfo sweep_info() {
     return {CFG::kCopies, CFG::kChains, CFG::kLds, std::max(1, CFG::kWavesPerSimd * 256 / CFG::kThreads), CFG::kBlk,
-            CFG::kFuse, CFG::kThreads};
+            CFG::kFuse, CFG::kThreads, CFG::kMirror};
 }
 
 ScanVariantInfo scan_variant_info_sweep(int v) {
@@ -75,31 +78,35 @@ ScanVariantInfo scan_variant_info_sweep(int v) {
     case 26: return sweep_info<ScanV26>();
     case 27: return sweep_info<ScanV27>();
     case 28: return sweep_info<ScanV28>();
+    case 29: return sweep_info<ScanV29>();
+    case 30: return sweep_info<ScanV30>();
     default: return {0, 0, 0, 0, 0, 0, 0};
     }
 }
 
 template <class T>
-static hipError_t sweep_launch(const ScanArgs& a, bool pred64, int grid, int block, hipStream_t s) {
-    if (pred64)
-        hipLaunchKernelGGL((cdc_scan_kernel<48, true, T>), dim3(grid), dim3(block), 0, s, a);
+static hipError_t sweep_launch(const ScanArgs& a, int pk, int grid, int block, hipStream_t s) {
+    if (pk == 1)
+        hipLaunchKernelGGL((cdc_scan_kernel<48, 1, T>), dim3(grid), dim3(block), 0, s, a);
+    else if (pk == 2 && T::kMirror)
+        hipLaunchKernelGGL((cdc_scan_kernel<48, T::kMirror ? 2 : 0, T>), dim3(grid), dim3(block), 0, s, a);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<48, false, T>), dim3(grid), dim3(block), 0, s, a);
+        hipLaunchKernelGGL((cdc_scan_kernel<48, 0, T>), dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_scan_sweep(const ScanArgs& a, int window, bool pred64, int variant, int grid, int block, hipStream_t s) {
+hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant, int grid, int block, hipStream_t s) {
     if (window != 48) return hipErrorInvalidValue;  // variants are built for the reference window only
     switch (variant) {
 #define SWEEP_CASE(id, T) \
-    case id: return sweep_launch<T>(a, pred64, grid, block, s);
+    case id: return sweep_launch<T>(a, pk, grid, block, s);
     SWEEP_CASE(1, ScanV1) SWEEP_CASE(2, ScanV2) SWEEP_CASE(3, ScanV3) SWEEP_CASE(4, ScanV4)
     SWEEP_CASE(5, ScanV5) SWEEP_CASE(6, ScanV6) SWEEP_CASE(7, ScanV7) SWEEP_CASE(8, ScanV8)
     SWEEP_CASE(9, ScanV9) SWEEP_CASE(10, ScanV10) SWEEP_CASE(15, ScanV15) SWEEP_CASE(16, ScanV16)
     SWEEP_CASE(17, ScanV17) SWEEP_CASE(19, ScanV19) SWEEP_CASE(20, ScanV20) SWEEP_CASE(21, ScanV21)
     SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3) SWEEP_CASE(14, ScanA4)
     SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15) SWEEP_CASE(22, ScanV22) SWEEP_CASE(26, ScanV26)
-    SWEEP_CASE(27, ScanV27) SWEEP_CASE(28, ScanV28)
+    SWEEP_CASE(27, ScanV27) SWEEP_CASE(28, ScanV28) SWEEP_CASE(29, ScanV29) SWEEP_CASE(30, ScanV30)
 #undef SWEEP_CASE
     default: return hipErrorInvalidValue;
     }
