@@ -2,6 +2,7 @@
 """Interleaved A/B of engine configurations in ONE process on the B1 workload (or BACKUP=1).
 
 usage: CONFIGS="base:;pf:SDFS_HASH_VARIANT=4;seg8k:SDFS_SEG_LEN=8192" python3 scripts/ab.py
+(MIN_SEG_KIB=2 MASK_BITS=11: the 4 KiB-mean chunk mix)
 Each config is `name:ENV=VAL,ENV=VAL` (environment read by the engine at creation; the sweep
 build is used by default so kernel variants can be selected).  The configurations run
 round-robin ROUNDS times on the same device-resident input; per-stage device times are
@@ -24,6 +25,9 @@ from sdfs_amd.device import DeviceBatch  # noqa: E402
 rounds = int(os.environ.get("ROUNDS", "10"))
 backup = os.environ.get("BACKUP") == "1"
 cfg = SdfsConfig.backup_volume() if backup else SdfsConfig()
+if os.environ.get("MASK_BITS"):  # e.g. the 4 KiB-mean mix: MIN_SEG_KIB=2 MASK_BITS=11
+    cfg = SdfsConfig(min_len=int(os.environ.get("MIN_SEG_KIB", "4")) * 1024 - 1,
+                     pred_mask=(1 << int(os.environ["MASK_BITS"])) - 1)
 buf_len = cfg.chunk_length
 nbuf = int(os.environ.get("NBUF", "102" if backup else "16384"))
 configs = []

@@ -413,18 +413,33 @@ __device__ __forceinline__ void sum_push(uint32_t (&s)[4], uint32_t& ncand, uint
 // the lanes' candidate summaries: the first candidate in [lo, hi] is the smallest candidate of
 // the first lane whose segment holds one there.  A step whose range touches an overflowed
 // segment searches the bitmap instead (same answer; the bitmap is complete).
+// QW (production): per-lane ascending candidate queue, one compare per cut; !QW (sweep variant
+// 31, the round-2 form): a min over the 8 summary slots per cut.
+template <bool QW = true>
 __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint32_t b, uint32_t lane,
                                                      const uint32_t (&sm)[4], uint32_t ncand, uint32_t ovf_off,
                                                      uint32_t seg_len, uint32_t* lhist) {
     const uint32_t len = a.uniform_len;
     const uint64_t word0 = ((uint64_t)b * len) >> 5;
     const uint32_t my_base = lane * seg_len;
-    uint32_t cand[kSumCands];
-#pragma unroll
-    for (uint32_t k = 0; k < kSumCands; k++) {
-        const uint32_t v = (sm[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-        cand[k] = v == 0xFFFFu ? 0xFFFFFFFFu : my_base + v;
+    // The lane's candidates as an ascending queue, smallest in the top slot: the summary holds the
+    // n = min(ncand, 8) candidates newest-lowest, so shift it up by 8 - n slots (0xFFFF fill).
+    // `head` is the smallest candidate not yet passed by the walk (cuts only move forward, so
+    // each candidate is popped once): per cut one compare instead of a min over all 8 slots.
+    uint32_t q0 = sm[0], q1 = sm[1], q2 = sm[2], q3 = sm[3];
+    {
+        const uint32_t sh = kSumCands - (ncand < kSumCands ? ncand : kSumCands);
+        if (sh & 4) { q3 = q1; q2 = q0; q1 = 0xFFFFFFFFu; q0 = 0xFFFFFFFFu; }
+        if (sh & 2) { q3 = q2; q2 = q1; q1 = q0; q0 = 0xFFFFFFFFu; }
+        if (sh & 1) {
+            q3 = __builtin_amdgcn_alignbit(q3, q2, 16);
+            q2 = __builtin_amdgcn_alignbit(q2, q1, 16);
+            q1 = __builtin_amdgcn_alignbit(q1, q0, 16);
+            q0 = (q0 << 16) | 0xFFFFu;
+        }
     }
+    auto head_of = [&](uint32_t top) { return (top >> 16) == 0xFFFFu ? 0xFFFFFFFFu : my_base + (top >> 16); };
+    uint32_t head = head_of(q3);
     const bool ovf = ncand > kSumCands;
     uint32_t start = 0, cnt = 0;
     while (start < len) {
@@ -434,14 +449,34 @@ __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint3
         int64_t k = -1;
         if (lo <= hi) {
             uint32_t best = 0xFFFFFFFFu;
+            bool search;
+            if constexpr (QW) {
+                for (;;) {  // drop every candidate the walk has passed
+                    const bool adv = head < lo;
+                    if (__ballot(adv) == 0) break;
+                    if (adv) {
+                        q3 = __builtin_amdgcn_alignbit(q3, q2, 16);
+                        q2 = __builtin_amdgcn_alignbit(q2, q1, 16);
+                        q1 = __builtin_amdgcn_alignbit(q1, q0, 16);
+                        q0 = (q0 << 16) | 0xFFFFu;
+                        head = head_of(q3);
+                    }
+                }
+                best = head <= hi ? head : 0xFFFFFFFFu;
+                search = ovf && head == 0xFFFFFFFFu;
+            } else {
 #pragma unroll
-            for (uint32_t j = 0; j < kSumCands; j++) {
-                const uint32_t c = cand[j];
-                if (c >= lo && c <= hi && c < best) best = c;
+                for (uint32_t j = 0; j < kSumCands; j++) {
+                    const uint32_t v = (sm[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                    const uint32_t c = v == 0xFFFFu ? 0xFFFFFFFFu : my_base + v;
+                    if (c >= lo && c <= hi && c < best) best = c;
+                }
+                search = ovf && best == 0xFFFFFFFFu;
             }
             // an overflowed segment's later candidates (after its 8th) are in the bitmap words
-            // the scan stored from block ovf_off on; a summary hit precedes all of them
-            if (ovf && best == 0xFFFFFFFFu) {
+            // the scan stored from block ovf_off on; they follow every summary candidate, so they
+            // matter only once the summary has none left in range
+            if (search) {
                 uint32_t x = my_base + ovf_off > lo ? my_base + ovf_off : lo;
                 const uint32_t seg_hi = my_base + seg_len - 1;
                 const uint32_t to = seg_hi < hi ? seg_hi : hi;
@@ -710,7 +745,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
                     for (int c = 0; c < NCH; c++) {
                         const uint64_t sc = seg0 + (uint64_t)c * blockDim.x;
                         if (sc < total)
-                            resolve_from_summary(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c], ovf_off[c], a.seg_len,
+                            resolve_from_summary<(CFG::kAbl & 128) == 0>(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c], ovf_off[c], a.seg_len,
                                                  lhist);
                     }
                 } else {
