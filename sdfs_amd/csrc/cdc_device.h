@@ -45,6 +45,12 @@ __device__ __forceinline__ uint32_t bitop3_and_or(uint32_t a, uint32_t b, uint32
 // push index rev8(j) sits at lo bits [64-d, 72-d) (jshift = 64 - d), and the LDS tables hold
 // bitrev64(push[rev8(x)]) / bitrev64(pop[rev8(x)]) at entry x (build_table_image, mirror).
 constexpr int kAblMirror = 64;
+// ABL bit kAblSgprPred (mirrored state, low-k zero predicate only): each position's compare goes
+// to an SGPR pair of its own (v_cmp_*_e64), eight positions are OR-ed on the scalar unit, and
+// only a group with a candidate in some lane shifts its eight bits in with v_addc (carry-in from
+// the SGPR pair); a group without one is a single v_lshlrev.  1 -> ~0.25 VALU per byte for the
+// candidate bits at a 12-bit predicate.
+constexpr int kAblSgprPred = 256;
 
 template <int P, int Q, int ABL = 0>
 __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
@@ -137,14 +143,28 @@ __device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t
 template <int W, int PK, int O, int ABL, int BLKW>
 __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& bits, const uint32_t (&cur)[BLKW],
                                           const uint32_t (&prev)[16], uint32_t c8, uint32_t push_base,
-                                          const uint8_t* tab, const ScanArgs& a) {
+                                          const uint8_t* tab, const ScanArgs& a, uint64_t (&gm)[8]) {
     constexpr int OLD = O - W;  // may be negative -> previous block
     constexpr int OI = OLD >= 0 ? OLD : OLD + 64;
     const uint32_t odw = OLD >= 0 ? cur[OI >> 2] : prev[OI >> 2];
     roll_step<(O & 3), (OI & 3), ABL>(lo, hi, cur[O >> 2], odw, c8, push_base, a.jshift, tab);
-    if constexpr (ABL & 4)
+    if constexpr (ABL & 4) {
         bits ^= lo;
-    else if constexpr ((ABL & kAblMirror) != 0)
+    } else if constexpr ((ABL & kAblSgprPred) != 0 && (ABL & kAblMirror) != 0 && PK == 2) {
+        asm("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(gm[O & 7]) : "s"(a.thr), "v"(hi));
+        if constexpr ((O & 7) == 7) {
+            const uint64_t any = (gm[0] | gm[1]) | (gm[2] | gm[3]) | (gm[4] | gm[5]) | (gm[6] | gm[7]);
+            if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    uint64_t co;
+                    asm volatile("v_addc_co_u32_e64 %0, %1, %0, %0, %2" : "+v"(bits), "=s"(co) : "s"(gm[p]));
+                }
+            } else {
+                bits <<= 8;
+            }
+        }
+    } else if constexpr ((ABL & kAblMirror) != 0)
         cand_shift<PK>(bits, hi, lo, a);
     else
         cand_shift<PK>(bits, lo, hi, a);
@@ -195,21 +215,22 @@ constexpr int kSchedGroup = SDFS_SCAN_SCHED_GROUP;  // bytes per scheduling regi
 template <int W, int PK, int O0, int O, int NCH, int ABL, int BLKW>
 __device__ __forceinline__ void word_steps(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
                                            const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
-                                           uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
+                                           uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a,
+                                           uint64_t (&gm)[NCH][8]) {
     if constexpr (O < O0 + 32) {
         if constexpr (NCH > 1 && ABL == 0) {
             bytes_multi<W, PK, O, NCH, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
         } else {
 #pragma unroll
             for (int c = 0; c < NCH; c++)
-                byte_step<W, PK, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a);
+                byte_step<W, PK, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a, gm[c]);
         }
         if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) {
             // keep the scheduler from hoisting every (chain-independent) pop read of the block
             // ahead of the rolling chain: that costs ~2 VGPRs per byte and spills.
             __builtin_amdgcn_sched_barrier(0);
         }
-        word_steps<W, PK, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+        word_steps<W, PK, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a, gm);
     }
 }
 
@@ -257,9 +278,10 @@ __device__ __forceinline__ void block_words(uint32_t (&words)[NCH][NW], uint32_t
                 for (int i = 8 * WI; i < 8 * WI + 8; i++) cur[c][i] = __builtin_bitreverse32(cur[c][i]);
         }
         uint32_t bits[NCH];
+        uint64_t gm[NCH][8];  // kAblSgprPred: the group's per-position compare masks (SGPR pairs)
 #pragma unroll
         for (int c = 0; c < NCH; c++) bits[c] = 0;
-        word_steps<W, PK, 32 * WI, 32 * WI, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
+        word_steps<W, PK, 32 * WI, 32 * WI, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a, gm);
 #pragma unroll
         for (int c = 0; c < NCH; c++) words[c][WI] = __builtin_bitreverse32(bits[c]);
         block_words<W, PK, WI + 1, NW, NCH, ABL, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
@@ -543,7 +565,7 @@ template <int W, int PK, class CFG>
 __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
     static_assert(!CFG::kMirror || (CFG::kChains == 1 && !CFG::kPrefetch), "mirrored state: one chain, no prefetch");
     static_assert(CFG::kMirror || PK != 2, "the one-compare predicate needs the mirrored state");
-    constexpr int MB = CFG::kMirror ? kAblMirror : 0;
+    constexpr int MB = (CFG::kMirror ? kAblMirror : 0) | (CFG::kAbl & kAblSgprPred);
     constexpr int NCH = CFG::kChains;
     constexpr int C = CFG::kCopies;
     constexpr int BLK = CFG::kBlk;

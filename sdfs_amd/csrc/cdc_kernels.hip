@@ -25,10 +25,11 @@ namespace sdfs {
 // 128-byte lines per lane per iteration, so no line is fetched twice), the split fast-path
 // body (ABL bit 16) and the cut walk fused into the epilogue from register summaries (FUSE 2).
 // Bit-reversed (mirrored) rolling state (cdc_device.h roll_step): a low-k-bit zero predicate is
-// one compare, 9.4 instead of 10.1 VALU per byte.
-// Interleaved A/B on MI355X against the alternatives is in DESIGN.md §7-8 (sweep variant 29 =
-// this configuration with the plain state).
-using ScanProd = ScanCfg<32, 1, false, 4, 16, 256, 2, kScanThreads, true>;
+// one compare, and each position's compare lands in an SGPR pair of its own so that only
+// 8-position groups with a candidate pay for shifting their bits in (kAblSgprPred): ~8.6 instead
+// of 10.1 VALU per byte.  Interleaved A/B on MI355X against the alternatives is in DESIGN.md
+// §7-8 (sweep variants 29 = plain state, 30 = mirrored without the SGPR masks).
+using ScanProd = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred, 256, 2, kScanThreads, true>;
 
 template <class CFG>
 constexpr ScanVariantInfo info_of() {
