@@ -28,16 +28,16 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz int32 ops/s
 # VALU instructions per input byte per lane (SQ_INSTS_VALU / (bytes / 64), rocprofv3 PMC of the
-# production kernels, profiles/r02/end/pmc_summary.json): scan 9.95 (10.8 before the bit-reversed
-# rolling state and the queue cut walk), SHA-256 22.4 (1423 per 64-byte block incl. one padding
-# block per chunk)
-OPS_PER_BYTE = {"cdc_scan": 9.95, "chunk_hash": 22.4}
+# production kernels, profiles/r02/end/pmc_summary.json): scan 9.17 (10.8 before the bit-reversed
+# rolling state, the SGPR-mask candidate bits and the queue cut walk), SHA-256 22.4 (1423 per
+# 64-byte block incl. one padding block per chunk)
+OPS_PER_BYTE = {"cdc_scan": 9.17, "chunk_hash": 22.4}
 # SIMD issue cycles per wave-byte: the ISA mix of each kernel's loop weighted by the measured issue
 # cost of each instruction (scripts/isa_microbench.hip, profiles/r01/isa_microbench.txt: 2.0 for
 # xor/and/shift, 2.2 bitop3, 2.4 add/addc, 3.6 alignbit/perm/add3); the clock the microbenchmark
 # calibrates to under full VALU load is 2.07 GHz.  valu_busy = issue cycles / (SIMDs x clock x time).
-# scan: 23.6 in the 256-byte block body + ~1.4 for the walk and block overhead
-VALU_CYCLES_PER_BYTE = {"cdc_scan": 25.0, "chunk_hash": 4180.0 / 64 * 1.008}
+# scan: 21.5 in the 256-byte block body + ~1.5 for the walk and block overhead
+VALU_CYCLES_PER_BYTE = {"cdc_scan": 23.0, "chunk_hash": 4180.0 / 64 * 1.008}
 SIMDS, VALU_CLOCK_HZ = 256 * 4, 2.07e9
 METRIC = "device-resident GiB/s CDC+fingerprint, 4 KiB-mean chunks, 1/2/4/8 MI355X"
 
