@@ -1065,6 +1065,13 @@ template <int ALGO, int ABL = 0, int BS = 256, bool PF = false, bool PRIO = fals
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1, 8)))
 void chunk_hash_kernel(HashArgs a) {
     const uint32_t i = blockIdx.x * BS + threadIdx.x;
+    if constexpr ((ABL & 64) != 0) {
+        // LDS as an occupancy governor (sweep): 15 KiB per workgroup, never read.  Alone on a CU the
+        // VGPRs still allow four waves per SIMD; next to a 512-thread scan workgroup (130 KiB) only
+        // two of these workgroups fit, i.e. two fingerprint waves per SIMD beside two scan waves.
+        __shared__ uint8_t lds_pad[15 * 1024];
+        if (i == 0xFFFFFFFFu) reinterpret_cast<volatile uint8_t*>(lds_pad)[threadIdx.x] = 0;
+    }
     if (i >= *a.total) return;
     if constexpr (PRIO) {
         const uint32_t nb = __builtin_amdgcn_readfirstlane(sha_blocks(a.clens[a.tasks[i]]));

@@ -148,6 +148,9 @@ hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant,
     case 15: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
     case 16: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
     case 10: hipLaunchKernelGGL((chunk_hash_kernel<0, 4, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 30:  // production kernel + 15 KiB of LDS per workgroup: co-resides 2 waves/SIMD with a 512-thread scan
+        hipLaunchKernelGGL((chunk_hash_kernel<0, 16 | 64, 256, true, true>), dim3(blocks), dim3(256), 0, s, a);
+        break;
     case 21:  // persistent grid with the production task body (true next-block prefetch)
         if (!a.wave_ctr || !a.persist_grid) return hipErrorInvalidValue;
         hipLaunchKernelGGL((chunk_hash_persistent_kernel<0, true, 16>), dim3(a.persist_grid), dim3(256), 0, s, a);
