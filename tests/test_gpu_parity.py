@@ -580,3 +580,70 @@ def test_config4_backup_per_gpu_share_16gib():
     _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 1, 900, [0, 204, 408])
     mean = nbuf * L / total
     assert 7000 < mean < 9000, mean
+
+
+_SCAN_VARIANT_CHECK = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, os.environ["ROOT"])
+from oracle import cdc_oracle as O
+from sdfs_amd import HipVariableSha256HashEngine, SdfsConfig
+from tests.test_gpu_parity import _dense_candidate_buffers
+nbuf, L = 32, 262144
+dense = _dense_candidate_buffers(nbuf, L)
+rnd = np.stack([O.synth(O.SYNTH_SEED, 7, b * L, L) for b in range(nbuf)])
+# ragged lengths too: the guarded tail blocks and the separate cut walk
+rl = [1, 47, 48, 300, 4095, 4097, 65537, 262143, 262144, 200003]
+rb = np.concatenate([O.synth(5, 3, 0, n) for n in rl])
+ro = np.concatenate([[0], np.cumsum(rl[:-1])]).astype(np.uint64)
+PRMS = ((0xFFF, 4095), (0x7FF, 2047), (0x1FFF, 4095), (0x5A5, 4095))
+exp = {}
+for mask, min_len in PRMS:
+    p = O.Params(min_len=min_len, pred_mask=mask)
+    exp[mask] = ([[O.chunk(h[b].tobytes(), p) for b in range(nbuf)] for h in (dense, rnd)],
+                 [O.chunk(rb[int(ro[b]): int(ro[b]) + n].tobytes(), p) for b, n in enumerate(rl)])
+for variant in (0, 29, 30, 31, 32):
+    os.environ["SDFS_SCAN_VARIANT"] = str(variant)  # read at create (tuning library only)
+    for mask, min_len in PRMS:
+        cfg = SdfsConfig(min_len=min_len, pred_mask=mask)
+        e = HipVariableSha256HashEngine(config=cfg)
+        # 32 buffers: the short-segment scan + separate cut walk of small batches; 1024 buffers
+        # (the 64 tiled 16 times): the fused one-wave-per-buffer scan and queue walk
+        for reps, host, ex in ((1, dense, exp[mask][0][0]), (1, rnd, exp[mask][0][1]),
+                               (16, np.concatenate([dense, rnd]), exp[mask][0][0] + exp[mask][0][1])):
+            big = np.tile(host, (reps, 1))
+            n = big.shape[0]
+            offs = np.arange(n, dtype=np.uint64) * L
+            c, st, ln, dg = e.chunk_batch(big.reshape(-1), offs, np.full(n, L, np.uint32))
+            for b in range(n):
+                es, el, ed = ex[b % len(ex)]
+                k = int(c[b])
+                assert st[b, :k].tolist() == es.tolist() and ln[b, :k].tolist() == el.tolist(), (variant, mask, n, b)
+                assert (dg[b, :k] == ed).all(), (variant, mask, n, b)
+        c, st, ln, dg = e.chunk_batch(rb, ro, np.array(rl, np.uint32))
+        for b, n in enumerate(rl):
+            es, el, ed = exp[mask][1][b]
+            k = int(c[b])
+            assert st[b, :k].tolist() == es.tolist() and ln[b, :k].tolist() == el.tolist(), (variant, mask, "ragged", b)
+            assert (dg[b, :k] == ed).all(), (variant, mask, "ragged", b)
+        e.destroy()
+print("scan variants ok")
+"""
+
+
+def test_scan_variants_agree():
+    """The scan forms the A/B measurements of DESIGN.md §4/§8 compare (production; 29 plain rolling
+    state; 30 mirrored state without the SGPR-mask candidate bits; 31 the round-2 cut walk; 32 =
+    the production form as a sweep variant) all give the oracle's chunks and digests: dense
+    candidate runs (summary overflow), random data, ragged lengths, 12-/11-/13-bit and pattern
+    predicates.  Non-production forms exist only in the tuning library, so this runs in a child
+    process bound to it."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ROOT=root, SDFS_CDC_LIB=_lib.TUNING_LIB)
+    r = subprocess.run([sys.executable, "-c", _SCAN_VARIANT_CHECK], capture_output=True, text=True, env=env,
+                       timeout=110, cwd=root)
+    assert r.returncode == 0 and "scan variants ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
