@@ -41,7 +41,8 @@ __device__ __forceinline__ uint32_t bitop3_and_or(uint32_t a, uint32_t b, uint32
 // held as hi:lo = R >> 32 : R.  fp << 8 becomes R >> 8, the incoming byte lands bit-reversed in
 // R's top byte, and fp bits 0..31 (the predicate's field) are hi bits 31..0 — so a low-k-bit
 // zero predicate is ONE compare (hi < 2^(32-k)) instead of v_and + v_cmp.  The data dwords are
-// bit-reversed once after their load (byte p of a dword becomes byte 3-p, bits reversed), the
+// bit-reversed in registers once, before their first position (block_words; byte p of a dword
+// becomes byte 3-p, bits reversed), the
 // push index rev8(j) sits at lo bits [64-d, 72-d) (jshift = 64 - d), and the LDS tables hold
 // bitrev64(push[rev8(x)]) / bitrev64(pop[rev8(x)]) at entry x (build_table_image, mirror).
 constexpr int kAblMirror = 64;
