@@ -30,7 +30,7 @@ struct ScanVariantInfo {
 };
 ScanVariantInfo scan_variant_info(int variant);
 
-constexpr int kMaxBins = 512;  // SHA work binning by block count (DESIGN.md "Load balance")
+constexpr int kMaxBins = 1024;  // SHA work binning by block count (exact counts up to maxLen 64 KiB)
 constexpr int kRecordBytes = 48;
 
 struct ResolveArgs {
