@@ -29,9 +29,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s mea
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz int32 ops/s
 # VALU instructions per input byte per lane (SQ_INSTS_VALU / (bytes / 64), rocprofv3 PMC of the
 # production kernels, profiles/r02/end/pmc_summary.json): scan 9.17 (10.8 before the bit-reversed
-# rolling state, the SGPR-mask candidate bits and the queue cut walk), SHA-256 22.4 (1423 per
+# rolling state, the SGPR-mask candidate bits and the queue cut walk), SHA-256 22.3 (~1 420 per
 # 64-byte block incl. one padding block per chunk)
-OPS_PER_BYTE = {"cdc_scan": 9.17, "chunk_hash": 22.4}
+OPS_PER_BYTE = {"cdc_scan": 9.17, "chunk_hash": 22.3}
 # SIMD issue cycles per wave-byte: the ISA mix of each kernel's loop weighted by the measured issue
 # cost of each instruction (scripts/isa_microbench.hip, profiles/r01/isa_microbench.txt: 2.0 for
 # xor/and/shift, 2.2 bitop3, 2.4 add/addc, 3.6 alignbit/perm/add3); the clock the microbenchmark
