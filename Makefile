@@ -12,7 +12,7 @@ TUNING_LIB := sdfs_amd/libsdfs_cdc_tuning.so
 SRCS := cdc_kernels cdc_engine dedup_index lz4_kernels map_emit aes_kernels
 OBJS := $(SRCS:%=build/%.o)
 TUNING_OBJS := $(SRCS:%=build/tuning/%.o) build/tuning/cdc_sweep.o
-HDRS := $(CSRC)/cdc_internal.h $(CSRC)/cdc_device.h $(CSRC)/host_queue.h $(CSRC)/stream_order.h $(wildcard include/*.h)
+HDRS := $(CSRC)/cdc_internal.h $(CSRC)/cdc_device.h $(CSRC)/host_queue.h $(CSRC)/engine_share.h $(CSRC)/stream_order.h $(wildcard include/*.h)
 
 all: $(LIB) tuning tools oracle
 
@@ -27,10 +27,10 @@ build/tuning/%.o: $(CSRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DSDFS_TUNING -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -ldl
 
 $(TUNING_LIB): $(TUNING_OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(TUNING_OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(TUNING_OBJS) -ldl
 
 # host-side harnesses: the multi-threaded getChunks driver (bench.py, GPU tests) and the JNI glue
 tools: tools/libsdfs_threads.so jni/libsdfs_cdc_jni.so tests/jni/libjni_stub.so

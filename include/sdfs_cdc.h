@@ -18,8 +18,25 @@
  * static singleton; the flush pools are Main.writeThreads wide, WritableCacheBuffer.java:100-104),
  * so every call is re-entrant and thread-safe.  Concurrent sdfs_cdc_get_chunks / sdfs_cdc_get_hash
  * calls are coalesced: each caller copies its bytes into a shared pinned staging slot, one GPU
- * pass serves the whole slot (up to two passes in flight), and each caller returns with its own
- * results (DESIGN.md "Host edge").  The product library reads no environment variables.
+ * pass serves the whole slot (up to four passes in flight per device), and each caller returns
+ * with its own results.  The product library reads no environment variables.
+ *
+ * Sharing (ABI 2): SDFS makes many engine instances — static singletons (SparseDedupFile.java:100,
+ * HashBlobArchive.java:140, FileIOServiceImpl.java:152), one-shot ones (HashStore.java:68) and a
+ * pool of one per concurrent write-accelerator caller (HashFunctionPool.java:73-86,
+ * WritableCacheBuffer.java:640,779).  sdfs_cdc_create therefore returns a HANDLE to a
+ * process-wide engine shared by every handle with the same parameters and device set: all of
+ * them feed the same coalescing queue(s).  sdfs_cdc_destroy ends one handle: its calls in
+ * progress finish first, later calls on it fail with SDFS_CDC_EINVAL, and the last handle of an
+ * engine releases the GPU resources.
+ *
+ * Devices (ABI 2): an engine spans a DEVICE SET (params.device / params.device_mask), one
+ * coalescing queue and lane set per GPU.  Host-buffer calls are spread over the set: a call that
+ * names its write stream (sdfs_cdc_get_chunks_stream; getChunks(buf, uuid)) goes to the device
+ * its stream key maps to, so one stream stays on one GPU; an unkeyed call goes to the least busy
+ * device; a batched call is split into contiguous shares, one per device, run concurrently.
+ * Device-resident calls run on the device that holds their data pointer.  The fingerprint tables
+ * of the devices are all-gathered in process over RCCL (sdfs_cdc_allgather_records).
  */
 #ifndef SDFS_CDC_H
 #define SDFS_CDC_H
@@ -31,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SDFS_CDC_ABI_VERSION 1
+#define SDFS_CDC_ABI_VERSION 2
 
 enum sdfs_cdc_status {
     SDFS_CDC_OK = 0,
@@ -64,9 +81,10 @@ typedef struct sdfs_cdc_params {
     uint64_t pred_value;
     uint32_t min_cmp;       /* enum sdfs_cdc_min_cmp */
     uint32_t hash_algo;     /* enum sdfs_cdc_hash_algo */
-    int32_t device;         /* HIP device ordinal */
+    int32_t device;         /* HIP device ordinal; -1 = every gfx950 device (a device set) */
     uint32_t flags;         /* SDFS_CDC_FLAG_*; 0 = defaults */
     uint64_t max_batch_bytes; /* host-batch staging per slot (pinned, two slots); 0 = default 256 MiB */
+    uint64_t device_mask;   /* ABI 2: bit i = HIP ordinal i in the device set (0 = use `device`) */
 } sdfs_cdc_params;
 
 /* flags: serve every getChunks / getHash call with its own GPU round trip instead of coalescing
@@ -106,6 +124,12 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out);
 int sdfs_cdc_destroy(sdfs_cdc_engine* e);
 const char* sdfs_cdc_last_error(void);
 
+/* The engine's device set: number of devices, and the HIP ordinal of set member i. */
+int sdfs_cdc_device_count(const sdfs_cdc_engine* e);
+int sdfs_cdc_device_ordinal(const sdfs_cdc_engine* e, int i);
+/* Live handles sharing this handle's engine (1 = not shared). */
+int sdfs_cdc_share_count(const sdfs_cdc_engine* e);
+
 /* ---- AbstractHashEngine accessors ---- */
 int sdfs_cdc_is_variable_length(const sdfs_cdc_engine* e);   /* isVariableLength(): 1 */
 int sdfs_cdc_get_max_len(const sdfs_cdc_engine* e);          /* getMaxLen(): Main.CHUNK_LENGTH (VariableSha256HashEngine.java:106-109) */
@@ -143,6 +167,19 @@ int sdfs_cdc_hash_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64
  * Synchronous for the caller; concurrent callers share GPU passes (see "Threading"). */
 int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, uint32_t* starts,
                         uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count);
+/* The same for a buffer of write stream `stream_key` (getChunks(buf, uuid): e.g. a hash of the
+ * file GUID the caller passes, SparseDedupFile.java:432): a device set serves every buffer of one
+ * stream on one device.  SDFS_CDC_NO_STREAM = no stream (least busy device). */
+#define SDFS_CDC_NO_STREAM UINT64_MAX
+int sdfs_cdc_get_chunks_stream(sdfs_cdc_engine* e, uint64_t stream_key, const uint8_t* buf, uint32_t len,
+                               uint32_t* starts, uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count);
+/* The same with the caller writing the buffer's bytes itself: fill(ctx, dst, len) is called once,
+ * on the calling thread, with dst = the space reserved for this call in the engine's pinned
+ * staging (so a JNI caller copies its byte[] once, GetByteArrayRegion straight into it).  A
+ * non-zero return from fill is returned by the call (its results are discarded). */
+typedef int (*sdfs_cdc_fill_fn)(void* ctx, uint8_t* dst, uint32_t len);
+int sdfs_cdc_get_chunks_fill(sdfs_cdc_engine* e, uint64_t stream_key, uint32_t len, sdfs_cdc_fill_fn fill, void* ctx,
+                             uint32_t* starts, uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count);
 /* Coalescing statistics since create: GPU passes launched and getChunks/getHash calls they served;
  * mean microseconds per pass spent filling (first call joined -> pass closed), waiting for the
  * callers' copies into pinned staging, and on the device (transfers + kernels). */
@@ -174,8 +211,22 @@ int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_
 int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes,
                                const uint64_t* d_offs, const uint32_t* d_lens, uint32_t nbuf,
                                uint64_t buffer_id_base, const sdfs_cdc_dev_out* out, void* stream);
-/* Block until the engine's own stream has drained. */
+/* Block until the engine's own stream (every device's) has drained. */
 int sdfs_cdc_stream_sync(sdfs_cdc_engine* e);
+
+/* ---- multi-GPU exchange: the set's fingerprint tables all-gathered in process
+ * over RCCL (xGMI), one communicator per device (ncclCommInitAll over the set).  Per device i of
+ * the set (set order): records[i] = its 48-byte records (sdfs_cdc_dev_out.records, room for
+ * records_cap[i]), d_totals[i] = their count (device u32, sdfs_cdc_dev_out.total), gathered[i] =
+ * the destination on device i (room for gathered_cap records), streams[i] = a hipStream_t of
+ * device i (NULL array = null streams).  First the counts are gathered and read back (counts[j],
+ * one small device->host copy: the call blocks for it), then every table is gathered padded to
+ * the largest count *stride: device j's records land at gathered[i] + j * *stride * 48.  The
+ * table gather is enqueued on streams[i] and the call returns.  Errors: ECAP when a table would
+ * not fit, ENODEV when RCCL cannot be loaded. */
+int sdfs_cdc_allgather_records(sdfs_cdc_engine* e, uint8_t* const* records, const uint64_t* records_cap,
+                               const uint32_t* const* d_totals, uint8_t* const* gathered, uint64_t gathered_cap,
+                               uint32_t* counts, uint64_t* stride, void* const* streams);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel of the
  * next runs (a ring of `nruns` event sets; 0 disables).  sdfs_cdc_kernel_times waits for the
@@ -187,6 +238,8 @@ int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns);
  * report 0.  Fewer events per run = less event overhead in a timed region. */
 int sdfs_cdc_set_timing_mask(sdfs_cdc_engine* e, int nruns, uint32_t stage_mask);
 int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int n);
+/* The same for device set member dev_index (sdfs_cdc_kernel_times = member 0). */
+int sdfs_cdc_kernel_times_on(sdfs_cdc_engine* e, int dev_index, const char** names, float* ms, int n);
 
 /* Synthetic input generator, device side: fills d_out[0..n) with byte
  * (offset+i) of stream `stream` (counter-based SplitMix64; same bytes as the CPU definition),

@@ -14,6 +14,7 @@ import java.io.IOException;
 import java.util.ArrayList;
 import java.util.Arrays;
 import java.util.List;
+import java.util.concurrent.locks.ReentrantReadWriteLock;
 
 import org.opendedup.sdfs.Main;
 
@@ -23,13 +24,18 @@ public final class HipVariableSha256HashEngine implements AbstractHashEngine {
     static { System.loadLibrary("sdfs_cdc_jni"); }   // links libsdfs_cdc.so
 
     private static final long POLY = 10923124345206883L;  // VariableSha256HashEngine.java:41
-    private volatile long handle;                          // sdfs_cdc_engine*
+    private long handle;                                   // sdfs_cdc_engine handle (guarded by lock)
     private final int hashLen;                             // 32, 20 or 16
+    // calls hold the read lock, destroy() the write lock: no call ever uses a destroyed handle
+    // (HashFunctionPool.destroyObject, HashFunctionPool.java:98-100, may race a borrower)
+    private final ReentrantReadWriteLock lock = new ReentrantReadWriteLock();
 
+    /** Every instance with the same parameters shares ONE native engine (all GPUs of the
+     *  "sdfs.hip.device" set: -1 = every gfx950 device, the default; an ordinal = that GPU). */
     public HipVariableSha256HashEngine(HASHTYPE ht) throws IOException {
         int algo = ht == HASHTYPE.HASH256 ? 0 : (ht == HASHTYPE.HASH160 ? 1 : 2);  // SDFS_CDC_*
         handle = nativeCreate(POLY, HashFunctionPool.bytesPerWindow, HashFunctionPool.minLen,
-                HashFunctionPool.maxLen, Main.CHUNK_LENGTH, algo, Integer.getInteger("sdfs.hip.device", 0));
+                HashFunctionPool.maxLen, Main.CHUNK_LENGTH, algo, Integer.getInteger("sdfs.hip.device", -1));
         hashLen = nativeDigestLen(handle);
     }
 
@@ -37,23 +43,39 @@ public final class HipVariableSha256HashEngine implements AbstractHashEngine {
     @Override public int getMaxLen() { return Main.CHUNK_LENGTH; }                 // :106-109
     @Override public int getMinLen() { return HashFunctionPool.minLen; }           // :111-114
     @Override public void setSeed(int seed) { }                                     // :116-120
-    @Override public synchronized void destroy() {
-        if (handle != 0) { nativeDestroy(handle); handle = 0; }
+    @Override public void destroy() {
+        lock.writeLock().lock();
+        try {
+            if (handle != 0) { nativeDestroy(handle); handle = 0; }
+        } finally { lock.writeLock().unlock(); }
     }
 
     @Override public byte[] getHash(byte[] data) {                                  // :58-67
         byte[] out = new byte[hashLen];
-        nativeGetHash(handle, data, out);   // throws IllegalStateException on a device error
+        lock.readLock().lock();
+        try {
+            if (handle == 0) throw new IllegalStateException("engine destroyed");
+            nativeGetHash(handle, data, out);   // throws IllegalStateException on a device error
+        } finally { lock.readLock().unlock(); }
         return out;
     }
 
     /** Thread-safe: SDFS's flush threads share one engine (SparseDedupFile.java:100); concurrent
      *  calls are coalesced into shared GPU passes inside the library. */
     @Override public List<Finger> getChunks(byte[] data, String uuid) throws IOException {  // :71-86
-        int cap = nativeSlotCap(handle, data.length);
-        int[] starts = new int[cap], lens = new int[cap];
-        byte[] digests = new byte[cap * hashLen];
-        int n = nativeGetChunks(handle, data, starts, lens, digests);  // IOException on failure
+        int[] starts, lens;
+        byte[] digests;
+        int n;
+        long key = uuid == null ? -1L : (uuid.hashCode() & 0xffffffffL);  // write-stream key
+        lock.readLock().lock();
+        try {
+            if (handle == 0) throw new IOException("engine destroyed");
+            int cap = nativeSlotCap(handle, data.length);
+            starts = new int[cap];
+            lens = new int[cap];
+            digests = new byte[cap * hashLen];
+            n = nativeGetChunks(handle, data, key, starts, lens, digests);  // IOException on failure
+        } finally { lock.readLock().unlock(); }
         ArrayList<Finger> al = new ArrayList<Finger>(n);
         for (int i = 0; i < n; i++) {
             Finger f = new Finger(uuid);
@@ -74,7 +96,7 @@ public final class HipVariableSha256HashEngine implements AbstractHashEngine {
     private static native void nativeDestroy(long h);
     private static native int nativeSlotCap(long h, int len);
     private static native int nativeDigestLen(long h);
-    private static native int nativeGetChunks(long h, byte[] data, int[] starts, int[] lens,
+    private static native int nativeGetChunks(long h, byte[] data, long key, int[] starts, int[] lens,
                                               byte[] digests) throws IOException;
     private static native int nativeGetHash(long h, byte[] data, byte[] out);
     private static native int nativeRegister(java.nio.ByteBuffer direct) throws IOException;

@@ -10,15 +10,22 @@
  *                    (failure -> IOException; the factory then logs fatal + System.exit(5),
  *                    HashFunctionPool.java:116-119)
  *   nativeGetChunks  getChunks(byte[], uuid) (VariableSha256HashEngine.java:71-86); a failure
- *                    throws java.io.IOException, as writeCache expects (SparseDedupFile.java:578-580)
+ *                    throws java.io.IOException, as writeCache expects (SparseDedupFile.java:578-580).
+ *                    The uuid's hash is the write-stream key: on a device set (all GPUs) one
+ *                    stream's buffers stay on one GPU.
  *   nativeGetHash    getHash(byte[]) (VariableSha256HashEngine.java:58-67)
  *   nativeRegister   page-locks a direct ByteBuffer the shim uses as a flush buffer
  *
  * Java arrays are copied in and out with Get/Set<Type>ArrayRegion rather than held with
  * GetPrimitiveArrayCritical: a getChunks call blocks for a GPU pass (~1 ms), and a JVM cannot
  * start a collection while any thread is inside a critical region, so 100+ flush threads holding
- * one would stall the collector.  The input copy lands in a per-thread native buffer (the engine
- * copies it into pinned staging from there).
+ * one would stall the collector.  getChunks copies its byte[] once, with GetByteArrayRegion
+ * straight into the engine's pinned staging (sdfs_cdc_get_chunks_fill); getHash goes through a
+ * per-thread native buffer.
+ *
+ * Every `new HipVariableSha256HashEngine` (static, pooled or one-shot) gets a handle to the ONE
+ * process-wide engine of its parameters (include/sdfs_cdc.h "Sharing"), so all of SDFS's engine
+ * instances feed the same coalescing queue(s).
  *
  * Built against jni/jni_min.h here (no JDK in this image); -DSDFS_USE_JDK_JNI uses the JDK's jni.h.
  */
@@ -136,10 +143,24 @@ JNIEXPORT jint JNICALL CLS(nativeDigestLen)(JNIEnv* env, jclass cls, jlong h) {
     return (jint)sdfs_cdc_digest_len(ENG(h));
 }
 
-/* Chunks data[0 .. data.length) into starts/lens (jint each) and digests (digest_len bytes each,
+/* The fill callback of sdfs_cdc_get_chunks_fill: the byte[] is copied ONCE, straight into the
+ * space the engine reserved for this call in its pinned staging. */
+struct fill_ctx {
+    JNIEnv* env;
+    jbyteArray data;
+};
+
+static int fill_from_array(void* ctx, uint8_t* dst, uint32_t len) {
+    struct fill_ctx* f = (struct fill_ctx*)ctx;
+    (*f->env)->GetByteArrayRegion(f->env, f->data, 0, (jsize)len, (jbyte*)dst);
+    return (*f->env)->ExceptionCheck(f->env) ? -1 : 0;
+}
+
+/* Chunks data[0 .. data.length) of write stream `key` (the uuid's hashCode as an unsigned 32-bit
+ * value, or -1 for none) into starts/lens (jint each) and digests (digest_len bytes each,
  * packed); returns the chunk count, or -1 with a pending IOException. */
-JNIEXPORT jint JNICALL CLS(nativeGetChunks)(JNIEnv* env, jclass cls, jlong h, jbyteArray data, jintArray starts,
-                                            jintArray lens, jbyteArray digests) {
+JNIEXPORT jint JNICALL CLS(nativeGetChunks)(JNIEnv* env, jclass cls, jlong h, jbyteArray data, jlong key,
+                                            jintArray starts, jintArray lens, jbyteArray digests) {
     (void)cls;
     sdfs_cdc_engine* e = ENG(h);
     if (!e || !data || !starts || !lens || !digests) {
@@ -149,21 +170,26 @@ JNIEXPORT jint JNICALL CLS(nativeGetChunks)(JNIEnv* env, jclass cls, jlong h, jb
     const jsize n = (*env)->GetArrayLength(env, data);
     const jsize cap = (*env)->GetArrayLength(env, starts);
     const int dl = sdfs_cdc_digest_len(e);
+    if (dl <= 0) {
+        throw_java(env, "java/io/IOException", sdfs_cdc_last_error());
+        return -1;
+    }
     if ((*env)->GetArrayLength(env, lens) < cap || (*env)->GetArrayLength(env, digests) < (jsize)((int64_t)cap * dl)) {
         throw_java(env, "java/io/IOException", "output arrays shorter than the chunk capacity");
         return -1;
     }
-    struct scratch* s = scratch_get((size_t)(n > 0 ? n : 1), (size_t)(cap > 0 ? cap : 1));
+    struct scratch* s = scratch_get(1, (size_t)(cap > 0 ? cap : 1));
     if (!s) {
         throw_java(env, "java/lang/OutOfMemoryError", "sdfs_cdc_jni scratch");
         return -1;
     }
-    (*env)->GetByteArrayRegion(env, data, 0, n, (jbyte*)s->in);
-    if ((*env)->ExceptionCheck(env)) return -1;
+    struct fill_ctx f = {env, data};
     uint32_t count = 0;
-    const int rc = sdfs_cdc_get_chunks(e, s->in, (uint32_t)n, s->st, s->ln, s->dg, (uint32_t)cap, &count);
+    const uint64_t stream = key < 0 ? SDFS_CDC_NO_STREAM : (uint64_t)key;
+    const int rc = sdfs_cdc_get_chunks_fill(e, stream, (uint32_t)n, fill_from_array, &f, s->st, s->ln, s->dg,
+                                            (uint32_t)cap, &count);
     if (rc != SDFS_CDC_OK) {
-        throw_java(env, "java/io/IOException", sdfs_cdc_last_error());
+        throw_java(env, "java/io/IOException", sdfs_cdc_last_error());  /* keeps a pending exception */
         return -1;
     }
     (*env)->SetIntArrayRegion(env, starts, 0, (jsize)count, (const jint*)s->st);

@@ -25,6 +25,9 @@ FLAG_DIRECT = 1  # SDFS_CDC_FLAG_DIRECT: no coalescing of concurrent getChunks/g
 SHA256, SHA256_160, MD5 = 0, 1, 2
 MIN_GT, MIN_GE = 0, 1
 RECORD_BYTES = 48
+NO_STREAM = (1 << 64) - 1  # SDFS_CDC_NO_STREAM
+ALL_DEVICES = -1           # sdfs_cdc_params.device: every gfx950 device
+FILL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32)
 
 
 class SdfsCdcError(IOError):
@@ -49,6 +52,7 @@ class Params(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("flags", ctypes.c_uint32),
         ("max_batch_bytes", ctypes.c_uint64),
+        ("device_mask", ctypes.c_uint64),
     ]
 
 
@@ -85,6 +89,17 @@ SIGNATURES = {
     "sdfs_cdc_slot_cap": (ctypes.c_uint32, [_vp, ctypes.c_uint64]),
     "sdfs_cdc_get_hash": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp]),
     "sdfs_cdc_get_chunks": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_uint32, _u32p]),
+    "sdfs_cdc_get_chunks_stream": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp, _vp,
+                                                  ctypes.c_uint32, _u32p]),
+    "sdfs_cdc_get_chunks_fill": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32, FILL_FN, _vp, _vp, _vp, _vp,
+                                                ctypes.c_uint32, _u32p]),
+    "sdfs_cdc_device_count": (ctypes.c_int, [_vp]),
+    "sdfs_cdc_device_ordinal": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "sdfs_cdc_share_count": (ctypes.c_int, [_vp]),
+    "sdfs_cdc_kernel_times_on": (ctypes.c_int, [_vp, ctypes.c_int, _P(ctypes.c_char_p), _P(ctypes.c_float),
+                                                ctypes.c_int]),
+    "sdfs_cdc_allgather_records": (ctypes.c_int, [_vp, _P(_vp), _u64p, _P(_vp), _P(_vp), ctypes.c_uint64, _u32p,
+                                                  _u64p, _P(_vp)]),
     "sdfs_cdc_get_chunks_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp,
                                                  ctypes.c_uint32]),
     "sdfs_cdc_run_device": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,

@@ -4,6 +4,7 @@
 // Drop-in for org.opendedup.hashing.AbstractHashEngine (AbstractHashEngine.java:24-39) as
 // implemented by VariableSha256HashEngine / VariableMD5HashEngine
 // (VariableSha256HashEngine.java:41-121, VariableMD5HashEngine.java:37-108).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,10 +15,12 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sdfs_cdc.h"
 #include "cdc_internal.h"
+#include "engine_share.h"
 #include "host_queue.h"
 
 using namespace sdfs;
@@ -226,7 +229,8 @@ struct QSlotDev {
 
 struct QueueBackend;
 
-struct sdfs_cdc_engine {
+struct DevEngine {
+    ~DevEngine();  // full teardown (the last handle of its set is gone)
     sdfs_cdc_params prm{};
     int degree = 0;
     int num_cus = 256;
@@ -299,6 +303,7 @@ int validate(const sdfs_cdc_params* p) {
     if (p->hash_algo > SDFS_CDC_MD5) return fail(SDFS_CDC_EINVAL, "bad hash_algo");
     if (p->pred_mask >> d) return fail(SDFS_CDC_EINVAL, "pred_mask has bits above the fp degree");
     if (p->flags & ~(uint32_t)SDFS_CDC_FLAG_DIRECT) return fail(SDFS_CDC_EINVAL, "unknown flags 0x%x", p->flags);
+    if (p->device < -1 && !p->device_mask) return fail(SDFS_CDC_EINVAL, "device %d (-1 = every gfx950 device)", p->device);
     return SDFS_CDC_OK;
 }
 
@@ -315,7 +320,7 @@ struct WsNeed {
 
 // Next workspace of the ring (or `own`, a queue slot's), sized for `nd`, ordered behind its
 // previous use on `s`.  Caller holds e->mu and has set the device.
-int ws_acquire(sdfs_cdc_engine* e, const WsNeed& nd, hipStream_t s, Workspace** out, Workspace* own = nullptr) {
+int ws_acquire(DevEngine* e, const WsNeed& nd, hipStream_t s, Workspace** out, Workspace* own = nullptr) {
     Workspace* w = own ? own : &e->ws[e->ws_next++ % kRing];
     const bool fits = w->bitmap.fits(nd.bitmap_words) && w->small.fits(kSmall + 8) &&
                       w->rec_base.fits(nd.rec_base) && w->tasks.fits(nd.tasks) &&
@@ -347,7 +352,7 @@ int ws_release(Workspace* w, hipStream_t s) {
 }
 
 // Records a start event for stage `kid` on stream `st` (timing runs only); returns the pair index.
-int t_begin(sdfs_cdc_engine* e, int kid, hipStream_t st) {
+int t_begin(DevEngine* e, int kid, hipStream_t st) {
     if (!e->run || !((e->timing_mask >> kid) & 1u)) return -1;
     const int i = (int)e->run->kid.size();
     if (2 * i + 1 >= kEvPerRun) return -1;
@@ -355,12 +360,12 @@ int t_begin(sdfs_cdc_engine* e, int kid, hipStream_t st) {
     (void)hipEventRecord(e->run->ev[2 * i], st);
     return i;
 }
-void t_end(sdfs_cdc_engine* e, int i, hipStream_t st) {
+void t_end(DevEngine* e, int i, hipStream_t st) {
     if (e->run && i >= 0) (void)hipEventRecord(e->run->ev[2 * i + 1], st);
 }
 
 // Workspace needs of one pipeline run.
-WsNeed pipeline_need(const sdfs_cdc_engine* e, uint64_t data_bytes, uint32_t nbuf, uint32_t uniform_len, uint32_t cap,
+WsNeed pipeline_need(const DevEngine* e, uint64_t data_bytes, uint32_t nbuf, uint32_t uniform_len, uint32_t cap,
                      uint64_t max_buf_len, uint32_t* sec_len_out, uint32_t* nsec_out, uint32_t* spec_cap_out) {
     WsNeed nd;
     nd.bitmap_words = ((data_bytes + 63) / 64) * 2 + 2;
@@ -383,7 +388,7 @@ WsNeed pipeline_need(const sdfs_cdc_engine* e, uint64_t data_bytes, uint32_t nbu
 // The device pipeline (scan [+ fused cut walk] | resolve, prefix, scatter, fingerprint) of one
 // batch, enqueued on `s` behind everything already there, on workspace `w` (acquired by the
 // caller).  Caller holds e->mu.
-int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
+int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
                  const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
                  const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, uint32_t sec_len, uint32_t nsec,
                  uint32_t spec_cap, uint32_t* ovf_to = nullptr) {
@@ -590,7 +595,7 @@ int run_pipeline(sdfs_cdc_engine* e, Workspace* w, const uint8_t* d_data, uint64
 // Validates a device-run request, acquires a workspace and runs the pipeline on `s`.  The
 // overflow flag of the run is left at *ovf_dev (device word, valid until the workspace's next
 // use) when ovf_dev != NULL.  Caller holds e->mu.
-int device_run(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
+int device_run(DevEngine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
                const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
                const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, const uint32_t** ovf_dev,
                Workspace* own = nullptr, uint32_t* ovf_to = nullptr) {
@@ -615,7 +620,7 @@ int device_run(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, c
 }
 
 // Fingerprints of n extents on workspace scratch (getHash in bulk).  Caller holds e->mu.
-int hash_extents(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
+int hash_extents(DevEngine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
                  const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, hipStream_t s,
                  Workspace* own = nullptr) {
     if (n_max == 0) return SDFS_CDC_OK;
@@ -672,7 +677,7 @@ bool host_range_pinned(const uint8_t* p, uint64_t n) {
 }
 
 // Results of the batch in slot `sl` (synchronises on it) -> the caller's arrays.
-int drain_slot(sdfs_cdc_engine* e, HostSlot& sl, uint32_t* counts, uint32_t* starts, uint32_t* lens_out,
+int drain_slot(DevEngine* e, HostSlot& sl, uint32_t* counts, uint32_t* starts, uint32_t* lens_out,
                uint8_t* digests, uint32_t cap) {
     sl.busy = false;
     HIP_TRY(hipEventSynchronize(sl.done));
@@ -702,7 +707,7 @@ int drain_slot(sdfs_cdc_engine* e, HostSlot& sl, uint32_t* counts, uint32_t* sta
 // pinned slot i%2 (copy_threads threads) while the GPU copies in and chunks batch i-1, and the
 // results of batch i-2 are unpacked once its slot is needed again.  H2D runs on its own
 // stream; pipeline and D2H on the engine stream.  Caller holds e->mu.
-int host_batch_impl(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
+int host_batch_impl(DevEngine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
                     uint32_t nbuf, uint32_t* counts, uint32_t* starts, uint32_t* lens_out, uint8_t* digests,
                     uint32_t cap) {
     // 256 MiB per slot: smaller batches leave most CUs idle and pay the per-batch fixed costs
@@ -818,7 +823,7 @@ int host_batch_impl(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* off
     return SDFS_CDC_OK;
 }
 
-int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t nbuf,
+int host_batch(DevEngine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t nbuf,
                uint32_t* counts, uint32_t* starts, uint32_t* lens_out, uint8_t* digests, uint32_t cap) {
     if (nbuf == 0) return SDFS_CDC_OK;
     const int rc = host_batch_impl(e, base, offs, lens, nbuf, counts, starts, lens_out, digests, cap);
@@ -831,7 +836,7 @@ int host_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, co
 }
 
 // Direct getHash (inputs larger than a queue slot, or the queue disabled).  Caller holds e->mu.
-int get_hash_direct(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest) {
+int get_hash_direct(DevEngine* e, const uint8_t* data, uint64_t len, uint8_t* digest) {
     hipStream_t s = e->stream;
     int rc = pinned_ensure(&e->pin_data, &e->pin_data_n, len + 256);
     if (rc) return rc;
@@ -868,14 +873,16 @@ int get_hash_direct(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8
 
 // ---- coalescing-queue backend (host_queue.h) ----
 struct QueueBackend {
-    sdfs_cdc_engine* e;
+    DevEngine* e;
     uint64_t slot_bytes;
     uint32_t max_reqs;
+    uint64_t max_req;  // largest request the queue takes (CoalescingQueue::Config::max_req_bytes)
 
     uint64_t out_entries;  // chunk slots of a slot's result image: sum over its requests of dcap
 
     // Everything a slot needs is allocated here, once: growing a device buffer later would free
-    // the old one, and hipFree waits for the whole device (every batch in flight).
+    // the old one, and hipFree waits for the whole device (every batch in flight).  (The pipeline
+    // still checks every need, ws_acquire.)
     int prepare(QSlot& s) {
         HIP_TRY(hipSetDevice(e->prm.device));
         auto* d = new QSlotDev();
@@ -897,6 +904,14 @@ struct QueueBackend {
         HIP_TRY(w.tasks.ensure(out_entries));
         HIP_TRY(w.seg_prefix.ensure(max_reqs + 1ull));
         HIP_TRY(w.x_scratch.ensure(kExtentScratchWords + 2ull * max_reqs));
+        // a request long enough for the sectioned cut walk travels in a slot of its own (admits),
+        // so one buffer's sections bound its speculative-walk scratch (pipeline_need)
+        if (const uint32_t sec = resolve_section_len(max_req, e->prm.max_len)) {
+            const uint64_t nsec = (max_req + sec - 1) / sec;
+            HIP_TRY(w.spec_starts.ensure(nsec * (sec / (e->first_off + 1) + 2)));
+            HIP_TRY(w.spec_cnt.ensure(nsec));
+            HIP_TRY(w.spec_next.ensure(nsec));
+        }
         HIP_TRY(hipEventCreateWithFlags(&d->kdone, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&d->ws.free_ev, hipEventDisableTiming));
         // touch the pinned staging once here, not inside some caller's first request
@@ -910,8 +925,12 @@ struct QueueBackend {
         return ((n * 4 + nout * 8 + 64 + 15) & ~15ull) + nout * 32 + nh * 32 + 64;
     }
 
+    // getChunks requests whose cut walk runs in sections (buffers of 4 MiB and more) travel alone
+    bool is_long(uint64_t len) const { return resolve_section_len(len, e->prm.max_len) != 0; }
+
     bool admits(const QSlot& s, const QReq& r) {
         if (r.kind != QReq::kChunks) return true;
+        if (!s.chunks.empty() && (is_long(r.len) || is_long(s.max_chunk_len))) return false;
         const uint64_t dcap = slot_cap_for(e->prm, std::max<uint64_t>(std::max<uint64_t>(s.max_chunk_len, r.len), 1));
         return (s.chunks.size() + 1) * dcap <= out_entries;
     }
@@ -1037,14 +1056,14 @@ namespace {
 
 // Starts the queue on first use.  Slot staging: 2 x CHUNK_LENGTH, at least 32 MiB (128 flush
 // buffers of 256 KiB; 40 MiB backup buffers get 80 MiB slots), at most 512 MiB.
-bool queue_ready(sdfs_cdc_engine* e) {
+bool queue_ready(DevEngine* e) {
     std::lock_guard<std::mutex> lk(e->q_init);
     if (e->q_state) return e->q_state > 0;
     const uint64_t slot = std::min<uint64_t>(std::max<uint64_t>(32ull << 20, 2ull * e->prm.chunk_length), 512ull << 20);
     // result image: room for every 64-byte-aligned request's worst-case chunk list at the
     // shortest chunk length, plus two slots of tail per request
     const uint64_t shortest = std::max<uint64_t>(1, std::min<uint64_t>(e->first_off + 1, e->prm.max_len));
-    e->qb.reset(new QueueBackend{e, slot, 1024, slot / shortest + 2ull * 1024});
+    e->qb.reset(new QueueBackend{e, slot, 1024, slot / 2, slot / shortest + 2ull * 1024});
     CoalescingQueue<QueueBackend>::Config c;
     c.nslots = kQueueSlots;
     c.lanes = kQueueInflight;
@@ -1083,44 +1102,20 @@ int queue_result(int rc, const QSlot* s) {
 
 }  // namespace
 
-extern "C" {
+// ---------------------------------------------------------------------------------------------
+// One device (DevEngine): what a handle's call runs on once the set has picked the device.
+// ---------------------------------------------------------------------------------------------
+namespace {
 
-int sdfs_cdc_abi_version(void) { return SDFS_CDC_ABI_VERSION; }
-
-const char* sdfs_cdc_last_error(void) { return g_last_error.c_str(); }
-
-int sdfs_cdc_params_default(sdfs_cdc_params* p, int backup_volume) {
-    if (!p) return fail(SDFS_CDC_EINVAL, "null params");
-    memset(p, 0, sizeof(*p));
-    p->poly = 10923124345206883ull;                        // VariableSha256HashEngine.java:41
-    p->window = 48;                                        // HashFunctionPool.java:51
-    p->min_len = 4 * 1024 - 1;                             // Main.java:189
-    p->max_len = backup_volume ? 128 * 1024 : 32 * 1024;   // VolumeConfigWriter.java:96,301
-    p->chunk_length = backup_volume ? 40960u * 1024 : 256u * 1024;  // VolumeConfigWriter.java:63,304
-    p->pred_mask = 0xFFF;                                  // SURVEY.md A.3 (knob; parity unpinned)
-    p->pred_value = 0;
-    p->min_cmp = SDFS_CDC_MIN_GT;
-    p->hash_algo = SDFS_CDC_SHA256;                        // VolumeConfigWriter.java:109
-    p->device = 0;
-    p->max_batch_bytes = 0;
-    return SDFS_CDC_OK;
-}
-
-int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
-    if (!out) return fail(SDFS_CDC_EINVAL, "null out");
-    *out = nullptr;
-    int rc = validate(p);
-    if (rc) return rc;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SDFS_CDC_ENODEV, "no HIP device");
-    if (p->device < 0 || p->device >= ndev) return fail(SDFS_CDC_ENODEV, "device %d of %d", p->device, ndev);
-    HIP_TRY(hipSetDevice(p->device));
+int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>* out) {
+    HIP_TRY(hipSetDevice(ordinal));
     hipDeviceProp_t prop;
-    HIP_TRY(hipGetDeviceProperties(&prop, p->device));
+    HIP_TRY(hipGetDeviceProperties(&prop, ordinal));
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return fail(SDFS_CDC_ENODEV, "device %d is %s, this build targets gfx950", p->device, prop.gcnArchName);
-    auto* e = new sdfs_cdc_engine();
+        return fail(SDFS_CDC_ENODEV, "device %d is %s, this build targets gfx950", ordinal, prop.gcnArchName);
+    std::unique_ptr<DevEngine> e(new DevEngine());
     e->prm = *p;
+    e->prm.device = ordinal;
     e->degree = poly_degree(p->poly);
     e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     e->first_off = p->min_cmp == SDFS_CDC_MIN_GT ? p->min_len : (p->min_len ? p->min_len - 1 : 0);
@@ -1138,10 +1133,7 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
         ok = ok && hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
     for (auto& w : e->ws) ok = ok && hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming) == hipSuccess;
-    if (!ok) {
-        sdfs_cdc_destroy(e);
-        return fail(SDFS_CDC_EHIP, "stream/event creation failed");
-    }
+    if (!ok) return fail(SDFS_CDC_EHIP, "stream/event creation failed");
 #ifdef SDFS_TUNING
     // measurement-only overrides (tuning library; the product library reads no environment)
     if (const char* v = getenv("SDFS_COPY_THREADS")) e->copy_threads = std::max(1, std::min(atoi(v), 64));
@@ -1157,126 +1149,100 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
         if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
             hipStreamCreateWithPriority(&e->s_scan, hipStreamNonBlocking, hi) != hipSuccess ||
             hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
-            sdfs_cdc_destroy(e);
+            hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
             return fail(SDFS_CDC_EHIP, "scan-priority stream creation failed");
-        }
     }
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif
     e->scan_info = scan_variant_info(e->scan_variant);
-    if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0) {
-        sdfs_cdc_destroy(e);
+    if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0)
         return fail(SDFS_CDC_EINVAL, "bad scan variant/segment length");
-    }
     std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies, e->scan_info.mirror != 0);
     if (e->zero_page.ensure(256) != hipSuccess || hipMemset(e->zero_page.p, 0, 256) != hipSuccess ||
         e->tab_image.ensure(img.size()) != hipSuccess ||
-        hipMemcpy(e->tab_image.p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
-        sdfs_cdc_destroy(e);
+        hipMemcpy(e->tab_image.p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess)
         return fail(SDFS_CDC_ENOMEM, "table upload failed");
-    }
-    *out = e;
+    *out = std::move(e);
     return SDFS_CDC_OK;
 }
 
-int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
-    if (!e) return SDFS_CDC_OK;
-    if (e->q) e->q->shutdown();  // joins the queue threads (no call may be in progress)
+}  // namespace
+
+DevEngine::~DevEngine() {
+    DevEngine* e = this;
+    if (e->q) e->q->shutdown();  // drains what was placed, joins the queue threads
     e->q.reset();
     e->qb.reset();
-    {
-        std::lock_guard<std::mutex> lk(e->mu);
-        (void)hipSetDevice(e->prm.device);
-        for (hipStream_t s : {e->stream, e->s_h2d, e->s_scan})
-            if (s) (void)hipStreamSynchronize(s);
-        for (hipStream_t s : e->qs)
-            if (s) (void)hipStreamSynchronize(s);
-        e->tab_image.release();
-        e->zero_page.release();
-        for (auto& w : e->ws) {
-            w.release_all();
-            if (w.free_ev) (void)hipEventDestroy(w.free_ev);
-        }
-        e->h_data.release();
-        e->o_starts.release();
-        e->o_digests.release();
-        e->x_data.release();
-        e->x_offs.release();
-        e->x_lens.release();
-        e->x_digests.release();
-        if (e->pin_data) (void)hipHostFree(e->pin_data);
-        for (auto& sl : e->hs) {
-            if (sl.pin_in) (void)hipHostFree(sl.pin_in);
-            if (sl.pin_out) (void)hipHostFree(sl.pin_out);
-            for (auto* b : {&sl.counts, &sl.starts, &sl.clens, &sl.total}) b->release();
-            sl.data.release();
-            sl.offs.release();
-            sl.lens.release();
-            sl.digests.release();
-            if (sl.h2d) (void)hipEventDestroy(sl.h2d);
-            if (sl.done) (void)hipEventDestroy(sl.done);
-        }
-        e->pool.reset();
-        for (auto& run : e->ev_runs)
-            for (auto& ev : run.ev)
-                if (ev) (void)hipEventDestroy(ev);
-        for (hipStream_t s : {e->stream, e->s_h2d, e->s_scan})
-            if (s) (void)hipStreamDestroy(s);
-        for (hipEvent_t ev : {e->ev_fork, e->ev_join})
-            if (ev) (void)hipEventDestroy(ev);
-        for (hipStream_t s : e->qs)
-            if (s) (void)hipStreamDestroy(s);
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipSetDevice(e->prm.device);
+    for (hipStream_t s : {e->stream, e->s_h2d, e->s_scan})
+        if (s) (void)hipStreamSynchronize(s);
+    for (hipStream_t s : e->qs)
+        if (s) (void)hipStreamSynchronize(s);
+    e->tab_image.release();
+    e->zero_page.release();
+    for (auto& w : e->ws) {
+        w.release_all();
+        if (w.free_ev) (void)hipEventDestroy(w.free_ev);
     }
-    delete e;
-    return SDFS_CDC_OK;
+    e->h_data.release();
+    e->o_starts.release();
+    e->o_digests.release();
+    e->x_data.release();
+    e->x_offs.release();
+    e->x_lens.release();
+    e->x_digests.release();
+    if (e->pin_data) (void)hipHostFree(e->pin_data);
+    for (auto& sl : e->hs) {
+        if (sl.pin_in) (void)hipHostFree(sl.pin_in);
+        if (sl.pin_out) (void)hipHostFree(sl.pin_out);
+        for (auto* b : {&sl.counts, &sl.starts, &sl.clens, &sl.total}) b->release();
+        sl.data.release();
+        sl.offs.release();
+        sl.lens.release();
+        sl.digests.release();
+        if (sl.h2d) (void)hipEventDestroy(sl.h2d);
+        if (sl.done) (void)hipEventDestroy(sl.done);
+    }
+    e->pool.reset();
+    for (auto& run : e->ev_runs)
+        for (auto& ev : run.ev)
+            if (ev) (void)hipEventDestroy(ev);
+    for (hipStream_t s : {e->stream, e->s_h2d, e->s_scan})
+        if (s) (void)hipStreamDestroy(s);
+    for (hipEvent_t ev : {e->ev_fork, e->ev_join})
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipStream_t s : e->qs)
+        if (s) (void)hipStreamDestroy(s);
 }
 
-int sdfs_cdc_is_variable_length(const sdfs_cdc_engine*) { return 1; }
-int sdfs_cdc_get_max_len(const sdfs_cdc_engine* e) { return e ? (int)e->prm.chunk_length : -1; }
-int sdfs_cdc_get_min_len(const sdfs_cdc_engine* e) { return e ? (int)e->prm.min_len : -1; }
-int sdfs_cdc_set_seed(sdfs_cdc_engine*, int) { return SDFS_CDC_OK; }
-int sdfs_cdc_digest_len(const sdfs_cdc_engine* e) { return e ? (int)e->digest_len : -1; }
-uint32_t sdfs_cdc_slot_cap(const sdfs_cdc_engine* e, uint64_t buf_len) { return e ? slot_cap_for(e->prm, buf_len) : 0; }
+namespace {
 
-int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
-                        uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base, const sdfs_cdc_dev_out* out,
-                        void* stream) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    if (!uniform_len)
-        return fail(SDFS_CDC_EINVAL, "sdfs_cdc_run_device: ragged layouts need sdfs_cdc_run_device_ragged");
-    (void)d_offs;
-    (void)d_lens;
+int dev_run_device(DevEngine* e, const uint8_t* d_data, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
+                   const sdfs_cdc_dev_out* out, hipStream_t s) {
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     return device_run(e, d_data, 0, nullptr, nullptr, nbuf, uniform_len, buffer_id_base, out, s, 0, nullptr);
 }
 
-int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
-                               const uint32_t* d_lens, uint32_t nbuf, uint64_t buffer_id_base,
-                               const sdfs_cdc_dev_out* out, void* stream) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+int dev_run_device_ragged(DevEngine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
+                          const uint32_t* d_lens, uint32_t nbuf, uint64_t buffer_id_base, const sdfs_cdc_dev_out* out,
+                          hipStream_t s) {
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     // the longest buffer is not known on the host: a few buffers sharing data_bytes are treated as
     // long (LDS-staged cut walk), many as their mean length
     const uint64_t max_len_hint = nbuf <= 4u * (uint32_t)e->num_cus ? data_bytes : data_bytes / (nbuf ? nbuf : 1);
     return device_run(e, d_data, data_bytes, d_offs, d_lens, nbuf, 0, buffer_id_base, out, s, max_len_hint, nullptr);
 }
 
-int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns) { return sdfs_cdc_set_timing_mask(e, nruns, 0xFFFFFFFFu); }
-
-int sdfs_cdc_set_timing_mask(sdfs_cdc_engine* e, int nruns, uint32_t stage_mask) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    if (nruns < 0 || nruns > 4096) return fail(SDFS_CDC_EINVAL, "timing slots %d", nruns);
+int dev_set_timing_mask(DevEngine* e, int nruns, uint32_t stage_mask) {
     std::lock_guard<std::mutex> lk(e->mu);
     e->timing_mask = stage_mask;
     HIP_TRY(hipSetDevice(e->prm.device));
     while ((int)e->ev_runs.size() < nruns) {
-        sdfs_cdc_engine::TimedRun r;
+        DevEngine::TimedRun r;
         r.ev.assign(kEvPerRun, nullptr);
         for (auto& ev : r.ev) HIP_TRY(hipEventCreate(&ev));
         e->ev_runs.push_back(std::move(r));
@@ -1286,8 +1252,7 @@ int sdfs_cdc_set_timing_mask(sdfs_cdc_engine* e, int nruns, uint32_t stage_mask)
     return SDFS_CDC_OK;
 }
 
-int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int n) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
+int dev_kernel_times(DevEngine* e, const char** names, float* ms, int n) {
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
     if (e->timing_slots == 0 || e->runs_recorded == 0) return 0;
@@ -1310,30 +1275,24 @@ int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int
     return k;
 }
 
-int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
-                              uint32_t nbuf, uint32_t* counts, uint32_t* starts, uint32_t* lens_out,
-                              uint8_t* digests, uint32_t cap) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    if (nbuf && (!base || !offs || !lens || !counts || !starts || !lens_out))
-        return fail(SDFS_CDC_EINVAL, "null argument");
+int dev_get_chunks_batch(DevEngine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t nbuf,
+                         uint32_t* counts, uint32_t* starts, uint32_t* lens_out, uint8_t* digests, uint32_t cap) {
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
     return host_batch(e, base, offs, lens, nbuf, counts, starts, lens_out, digests, cap);
 }
 
-int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, uint32_t* starts, uint32_t* lens,
-                        uint8_t* digests, uint32_t cap, uint32_t* count) {
-    if (!e || !count) return fail(SDFS_CDC_EINVAL, "null argument");
-    *count = 0;
-    if (len == 0) return SDFS_CDC_OK;  // an empty byte[] yields no Finger
-    if (!buf || !starts || !lens) return fail(SDFS_CDC_EINVAL, "null buffer");
+// getChunks of one buffer whose `len` bytes `fill` writes (into the queue's pinned staging when
+// the queue takes the request, else into a temporary buffer for the direct path).
+template <class Fill>
+int dev_get_chunks(DevEngine* e, uint32_t len, Fill&& fill, uint32_t* starts, uint32_t* lens, uint8_t* digests,
+                   uint32_t cap, uint32_t* count) {
     if (queue_ready(e) && e->q->accepts(len)) {
         QReq r;
         r.kind = QReq::kChunks;
-        r.src = buf;
         r.len = len;
         const uint32_t dl = e->digest_len;
-        const int rc = e->q->run(r, [&](const QSlot& s, const QReq& q, int status) -> int {
+        const int rc = e->q->run_fill(r, fill, [&](const QSlot& s, const QReq& q, int status) -> int {
             if (status) return queue_result(status, &s);
             const auto* d = static_cast<const QSlotDev*>(s.dev);
             const uint32_t* pc = reinterpret_cast<const uint32_t*>(d->pin_out);
@@ -1351,15 +1310,17 @@ int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, ui
         });
         return rc == kQueueStopped || rc == kQueueTooBig ? queue_result(rc, nullptr) : rc;
     }
+    std::unique_ptr<uint8_t[]> tmp(new (std::nothrow) uint8_t[len]);
+    if (!tmp) return fail(SDFS_CDC_ENOMEM, "getChunks: %u bytes of host memory", len);
+    const int frc = fill(tmp.get());
+    if (frc) return frc;
     const uint64_t off = 0;
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
-    return host_batch(e, buf, &off, &len, 1, count, starts, lens, digests, cap);
+    return host_batch(e, tmp.get(), &off, &len, 1, count, starts, lens, digests, cap);
 }
 
-int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest) {
-    if (!e || !digest || (len && !data)) return fail(SDFS_CDC_EINVAL, "null argument");
-    if (len > 0xFFFFFFFFull) return fail(SDFS_CDC_EINVAL, "getHash input > 4 GiB");
+int dev_get_hash(DevEngine* e, const uint8_t* data, uint64_t len, uint8_t* digest) {
     if (queue_ready(e) && e->q->accepts(len)) {
         QReq r;
         r.kind = QReq::kHash;
@@ -1379,53 +1340,8 @@ int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uin
     return get_hash_direct(e, data, len, digest);
 }
 
-int sdfs_cdc_queue_stats(sdfs_cdc_engine* e, uint64_t* batches, uint64_t* requests) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    std::lock_guard<std::mutex> lk(e->q_init);
-    if (batches) *batches = e->q ? e->q->batches() : 0;
-    if (requests) *requests = e->q ? e->q->requests() : 0;
-    return SDFS_CDC_OK;
-}
-
-int sdfs_cdc_queue_timing(sdfs_cdc_engine* e, double* fill_us, double* copy_us, double* device_us) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    std::lock_guard<std::mutex> lk(e->q_init);
-    if (e->q) {
-        e->q->timing(fill_us, copy_us, device_us);
-    } else {
-        if (fill_us) *fill_us = 0;
-        if (copy_us) *copy_us = 0;
-        if (device_us) *device_us = 0;
-    }
-    return SDFS_CDC_OK;
-}
-
-int sdfs_cdc_host_register(void* p, uint64_t n) {
-    if (!p || !n) return fail(SDFS_CDC_EINVAL, "null or empty region");
-    HIP_TRY(hipHostRegister(p, n, hipHostRegisterDefault));
-    return SDFS_CDC_OK;
-}
-
-int sdfs_cdc_host_unregister(void* p) {
-    if (!p) return fail(SDFS_CDC_EINVAL, "null region");
-    HIP_TRY(hipHostUnregister(p));
-    return SDFS_CDC_OK;
-}
-
-int sdfs_cdc_hash_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
-                         const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, void* stream) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    if (n_max && (!d_data || !d_offs || !d_lens || !d_digests)) return fail(SDFS_CDC_EINVAL, "null argument");
-    std::lock_guard<std::mutex> lk(e->mu);
-    HIP_TRY(hipSetDevice(e->prm.device));
-    return hash_extents(e, d_data, d_offs, d_lens, d_count, n_max, d_digests, reinterpret_cast<hipStream_t>(stream));
-}
-
-int sdfs_cdc_get_hash_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
-                            uint32_t n, uint8_t* digests) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    if (n == 0) return SDFS_CDC_OK;
-    if (!base || !offs || !lens || !digests) return fail(SDFS_CDC_EINVAL, "null argument");
+int dev_get_hash_batch(DevEngine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t n,
+                       uint8_t* digests) {
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->prm.device));
     hipStream_t s = e->stream;
@@ -1459,19 +1375,527 @@ int sdfs_cdc_get_hash_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint6
     return SDFS_CDC_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Handles and shared sets (engine_share.h): the C-ABI below.
+// ---------------------------------------------------------------------------------------------
+typedef Registry<DevEngine> Reg;
+typedef Handle<DevEngine> H;
+typedef SharedSet<DevEngine> Set;
+
+Reg& reg() {
+    static Reg* r = new Reg();  // never destroyed: no engine teardown runs after the HIP runtime's exit
+    return *r;
+}
+
+// The gfx950 ordinals a parameter block names: device_mask (bit i = ordinal i) when set, else
+// `device` (>= 0), else (-1) every gfx950 device.
+int device_set(const sdfs_cdc_params* p, std::vector<int>* ords) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return fail(SDFS_CDC_ENODEV, "no HIP device");
+    }
+    ords->clear();
+    if (p->device_mask) {
+        for (int i = 0; i < 64; i++)
+            if ((p->device_mask >> i) & 1) {
+                if (i >= ndev) return fail(SDFS_CDC_ENODEV, "device_mask names device %d of %d", i, ndev);
+                ords->push_back(i);
+            }
+        return SDFS_CDC_OK;
+    }
+    if (p->device >= 0) {
+        if (p->device >= ndev) return fail(SDFS_CDC_ENODEV, "device %d of %d", p->device, ndev);
+        ords->push_back(p->device);
+        return SDFS_CDC_OK;
+    }
+    if (p->device != -1) return fail(SDFS_CDC_EINVAL, "device %d (-1 = every gfx950 device)", p->device);
+    for (int i = 0; i < ndev; i++) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, i) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+            ords->push_back(i);
+    }
+    if (ords->empty()) return fail(SDFS_CDC_ENODEV, "no gfx950 device among %d", ndev);
+    return SDFS_CDC_OK;
+}
+
+// Engines are shared between handles whose parameters (other than the device fields) and device
+// sets are equal.
+std::string share_key(const sdfs_cdc_params* p, const std::vector<int>& ords) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%llx/%u/%u/%u/%u/%llx/%llx/%u/%u/%x/%llx|",
+             (unsigned long long)p->poly, p->window, p->min_len, p->max_len, p->chunk_length,
+             (unsigned long long)p->pred_mask, (unsigned long long)p->pred_value, p->min_cmp, p->hash_algo, p->flags,
+             (unsigned long long)p->max_batch_bytes);
+    std::string k(buf);
+    for (int o : ords) k += std::to_string(o) + ",";
+    return k;
+}
+
+#define USE_OR_FAIL(u, e)                                                            \
+    Reg::Use u(reg(), e);                                                            \
+    if (!u.ok()) return fail(SDFS_CDC_EINVAL, "not a live engine handle");
+
+// The set's device holding device pointer p (set order index); a set of one takes it as is.
+int dev_of_ptr(Set& s, const void* p, size_t* idx) {
+    *idx = 0;
+    if (s.ndev() == 1) return SDFS_CDC_OK;
+    hipPointerAttribute_t a;
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(SDFS_CDC_EINVAL, "not a device pointer: %p", p);
+    }
+    for (size_t i = 0; i < s.ndev(); i++)
+        if (s.ordinals[i] == a.device) {
+            *idx = i;
+            return SDFS_CDC_OK;
+        }
+    return fail(SDFS_CDC_EINVAL, "pointer %p is on device %d, outside this engine's device set", p, a.device);
+}
+
+// ---- in-process RCCL all-gather of the fingerprint tables ----
+// RCCL is opened on first use (dlopen), so the library loads, and serves every other call,
+// without it; the exchange itself fails loudly when it is missing.
+struct RcclApi {
+    typedef int (*init_all_t)(void**, int, const int*);
+    typedef int (*all_gather_t)(const void*, void*, size_t, int, void*, hipStream_t);
+    typedef int (*group_t)(void);
+    typedef int (*destroy_t)(void*);
+    typedef const char* (*errstr_t)(int);
+    init_all_t init_all = nullptr;
+    all_gather_t all_gather = nullptr;
+    group_t group_start = nullptr, group_end = nullptr;
+    destroy_t destroy = nullptr;
+    errstr_t errstr = nullptr;
+};
+constexpr int kNcclUint8 = 1, kNcclUint32 = 3;  // ncclDataType_t (rccl.h)
+
+const RcclApi* rccl_api() {
+    static RcclApi api;
+    static std::once_flag once;
+    static bool ok = false;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        api.init_all = (RcclApi::init_all_t)dlsym(h, "ncclCommInitAll");
+        api.all_gather = (RcclApi::all_gather_t)dlsym(h, "ncclAllGather");
+        api.group_start = (RcclApi::group_t)dlsym(h, "ncclGroupStart");
+        api.group_end = (RcclApi::group_t)dlsym(h, "ncclGroupEnd");
+        api.destroy = (RcclApi::destroy_t)dlsym(h, "ncclCommDestroy");
+        api.errstr = (RcclApi::errstr_t)dlsym(h, "ncclGetErrorString");
+        ok = api.init_all && api.all_gather && api.group_start && api.group_end && api.destroy && api.errstr;
+    });
+    return ok ? &api : nullptr;
+}
+
+// Per set: one communicator per device (ncclCommInitAll over the set's ordinals) and a small
+// device buffer per device for the gathered counts.
+struct Coll {
+    std::vector<void*> comms;
+    std::vector<uint32_t*> d_counts;  // [ndev] u32 on each device
+    uint32_t* h_counts = nullptr;     // pinned [ndev]
+    std::vector<int> ords;
+    ~Coll() {
+        const RcclApi* api = rccl_api();
+        for (size_t i = 0; i < comms.size(); i++)
+            if (comms[i] && api) api->destroy(comms[i]);
+        for (size_t i = 0; i < d_counts.size(); i++)
+            if (d_counts[i]) {
+                (void)hipSetDevice(ords[i]);
+                (void)hipFree(d_counts[i]);
+            }
+        if (h_counts) (void)hipHostFree(h_counts);
+    }
+};
+
+#define NCCL_TRY(api, expr)                                                                         \
+    do {                                                                                            \
+        const int _r = (expr);                                                                      \
+        if (_r != 0) return fail(SDFS_CDC_EHIP, "%s failed: %s", #expr, (api)->errstr(_r));          \
+    } while (0)
+
+int coll_ready(Set& s, Coll** out) {
+    std::lock_guard<std::mutex> lk(s.coll_mu);
+    if (s.coll) {
+        *out = static_cast<Coll*>(s.coll.get());
+        return SDFS_CDC_OK;
+    }
+    const RcclApi* api = rccl_api();
+    if (!api) return fail(SDFS_CDC_ENODEV, "RCCL (librccl.so.1) not loadable: %s", dlerror());
+    std::shared_ptr<Coll> c(new Coll());
+    const int n = (int)s.ndev();
+    c->ords = s.ordinals;
+    c->comms.assign(n, nullptr);
+    c->d_counts.assign(n, nullptr);
+    NCCL_TRY(api, api->init_all(c->comms.data(), n, s.ordinals.data()));
+    for (int i = 0; i < n; i++) {
+        HIP_TRY(hipSetDevice(s.ordinals[i]));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_counts[i]), 4ull * n));
+    }
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), 4ull * n, hipHostMallocDefault));
+    s.coll = c;
+    *out = c.get();
+    return SDFS_CDC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdfs_cdc_abi_version(void) { return SDFS_CDC_ABI_VERSION; }
+
+const char* sdfs_cdc_last_error(void) { return g_last_error.c_str(); }
+
+int sdfs_cdc_params_default(sdfs_cdc_params* p, int backup_volume) {
+    if (!p) return fail(SDFS_CDC_EINVAL, "null params");
+    memset(p, 0, sizeof(*p));
+    p->poly = 10923124345206883ull;                        // VariableSha256HashEngine.java:41
+    p->window = 48;                                        // HashFunctionPool.java:51
+    p->min_len = 4 * 1024 - 1;                             // Main.java:189
+    p->max_len = backup_volume ? 128 * 1024 : 32 * 1024;   // VolumeConfigWriter.java:96,301
+    p->chunk_length = backup_volume ? 40960u * 1024 : 256u * 1024;  // VolumeConfigWriter.java:63,304
+    p->pred_mask = 0xFFF;                                  // SURVEY.md A.3 (knob; parity unpinned)
+    p->pred_value = 0;
+    p->min_cmp = SDFS_CDC_MIN_GT;
+    p->hash_algo = SDFS_CDC_SHA256;                        // VolumeConfigWriter.java:109
+    p->device = 0;
+    p->max_batch_bytes = 0;
+    p->device_mask = 0;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
+    if (!out) return fail(SDFS_CDC_EINVAL, "null out");
+    *out = nullptr;
+    int rc = validate(p);
+    if (rc) return rc;
+    std::vector<int> ords;
+    rc = device_set(p, &ords);
+    if (rc) return rc;
+    H* h = nullptr;
+    rc = reg().create(share_key(p, ords), ords,
+                      [p](int ord, std::unique_ptr<DevEngine>* d) { return dev_create(p, ord, d); }, &h);
+    if (rc) return rc;
+    *out = reinterpret_cast<sdfs_cdc_engine*>(h);
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
+    if (!e) return SDFS_CDC_OK;
+    if (!reg().destroy(reinterpret_cast<H*>(e))) return fail(SDFS_CDC_EINVAL, "not a live engine handle");
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_device_count(const sdfs_cdc_engine* e) {
+    USE_OR_FAIL(u, e);
+    return (int)u.set().ndev();
+}
+
+int sdfs_cdc_device_ordinal(const sdfs_cdc_engine* e, int i) {
+    USE_OR_FAIL(u, e);
+    if (i < 0 || (size_t)i >= u.set().ndev()) return fail(SDFS_CDC_EINVAL, "device index %d", i);
+    return u.set().ordinals[i];
+}
+
+int sdfs_cdc_share_count(const sdfs_cdc_engine* e) {
+    USE_OR_FAIL(u, e);
+    return reg().refs_of(u.set());
+}
+
+int sdfs_cdc_is_variable_length(const sdfs_cdc_engine* e) {
+    USE_OR_FAIL(u, e);
+    return 1;
+}
+int sdfs_cdc_get_max_len(const sdfs_cdc_engine* e) {
+    Reg::Use u(reg(), e);
+    return u.ok() ? (int)u.set().devs[0]->prm.chunk_length : -1;
+}
+int sdfs_cdc_get_min_len(const sdfs_cdc_engine* e) {
+    Reg::Use u(reg(), e);
+    return u.ok() ? (int)u.set().devs[0]->prm.min_len : -1;
+}
+int sdfs_cdc_set_seed(sdfs_cdc_engine* e, int) {
+    USE_OR_FAIL(u, e);
+    return SDFS_CDC_OK;
+}
+int sdfs_cdc_digest_len(const sdfs_cdc_engine* e) {
+    Reg::Use u(reg(), e);
+    return u.ok() ? (int)u.set().devs[0]->digest_len : -1;
+}
+uint32_t sdfs_cdc_slot_cap(const sdfs_cdc_engine* e, uint64_t buf_len) {
+    Reg::Use u(reg(), e);
+    return u.ok() ? slot_cap_for(u.set().devs[0]->prm, buf_len) : 0;
+}
+
+int sdfs_cdc_run_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
+                        uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base, const sdfs_cdc_dev_out* out,
+                        void* stream) {
+    USE_OR_FAIL(u, e);
+    if (!uniform_len)
+        return fail(SDFS_CDC_EINVAL, "sdfs_cdc_run_device: ragged layouts need sdfs_cdc_run_device_ragged");
+    (void)d_offs;
+    (void)d_lens;
+    size_t i;
+    const int rc = dev_of_ptr(u.set(), d_data, &i);
+    if (rc) return rc;
+    return dev_run_device(u.set().devs[i].get(), d_data, nbuf, uniform_len, buffer_id_base, out,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
+int sdfs_cdc_run_device_ragged(sdfs_cdc_engine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
+                               const uint32_t* d_lens, uint32_t nbuf, uint64_t buffer_id_base,
+                               const sdfs_cdc_dev_out* out, void* stream) {
+    USE_OR_FAIL(u, e);
+    size_t i;
+    const int rc = dev_of_ptr(u.set(), d_data, &i);
+    if (rc) return rc;
+    return dev_run_device_ragged(u.set().devs[i].get(), d_data, data_bytes, d_offs, d_lens, nbuf, buffer_id_base, out,
+                                 reinterpret_cast<hipStream_t>(stream));
+}
+
+int sdfs_cdc_set_timing(sdfs_cdc_engine* e, int nruns) { return sdfs_cdc_set_timing_mask(e, nruns, 0xFFFFFFFFu); }
+
+int sdfs_cdc_set_timing_mask(sdfs_cdc_engine* e, int nruns, uint32_t stage_mask) {
+    USE_OR_FAIL(u, e);
+    if (nruns < 0 || nruns > 4096) return fail(SDFS_CDC_EINVAL, "timing slots %d", nruns);
+    for (auto& d : u.set().devs) {
+        const int rc = dev_set_timing_mask(d.get(), nruns, stage_mask);
+        if (rc) return rc;
+    }
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_kernel_times_on(sdfs_cdc_engine* e, int dev_index, const char** names, float* ms, int n) {
+    USE_OR_FAIL(u, e);
+    if (dev_index < 0 || (size_t)dev_index >= u.set().ndev()) return fail(SDFS_CDC_EINVAL, "device index %d", dev_index);
+    return dev_kernel_times(u.set().devs[dev_index].get(), names, ms, n);
+}
+
+int sdfs_cdc_kernel_times(sdfs_cdc_engine* e, const char** names, float* ms, int n) {
+    return sdfs_cdc_kernel_times_on(e, 0, names, ms, n);
+}
+
+int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
+                              uint32_t nbuf, uint32_t* counts, uint32_t* starts, uint32_t* lens_out,
+                              uint8_t* digests, uint32_t cap) {
+    USE_OR_FAIL(u, e);
+    if (nbuf && (!base || !offs || !lens || !counts || !starts || !lens_out))
+        return fail(SDFS_CDC_EINVAL, "null argument");
+    Set& s = u.set();
+    // Contiguous shares of the buffers, one per device, run concurrently (every buffer is chunked
+    // from fresh state, so a share is an independent batch); at least kShareMin buffers per device.
+    constexpr uint32_t kShareMin = 64;
+    const uint32_t k = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(s.ndev(), nbuf / kShareMin));
+    if (k == 1) {
+        const size_t i = Reg::pick(s, false, 0);
+        Reg::Load ld(s, i);
+        return dev_get_chunks_batch(s.devs[i].get(), base, offs, lens, nbuf, counts, starts, lens_out, digests, cap);
+    }
+    const uint32_t dl = s.devs[0]->digest_len;
+    std::vector<int> rcs(k, 0);
+    std::vector<std::string> errs(k);
+    auto share = [&](uint32_t d) {
+        Reg::Load ld(s, d);
+        const uint32_t b0 = share_begin(nbuf, k, d), b1 = share_begin(nbuf, k, d + 1);
+        const uint64_t o = (uint64_t)b0 * cap;
+        rcs[d] = dev_get_chunks_batch(s.devs[d].get(), base, offs + b0, lens + b0, b1 - b0, counts + b0, starts + o,
+                                      lens_out + o, digests ? digests + o * dl : nullptr, cap);
+        if (rcs[d]) errs[d] = g_last_error;
+    };
+    std::vector<std::thread> th;
+    for (uint32_t d = 1; d < k; d++) th.emplace_back(share, d);
+    share(0);
+    for (auto& t : th) t.join();
+    for (uint32_t d = 0; d < k; d++)
+        if (rcs[d]) return fail(rcs[d], "device %d: %s", s.ordinals[d], errs[d].c_str());
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_get_chunks_fill(sdfs_cdc_engine* e, uint64_t stream_key, uint32_t len, sdfs_cdc_fill_fn fill, void* ctx,
+                             uint32_t* starts, uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count) {
+    if (!count) return fail(SDFS_CDC_EINVAL, "null argument");
+    *count = 0;
+    USE_OR_FAIL(u, e);
+    if (len == 0) return SDFS_CDC_OK;  // an empty byte[] yields no Finger
+    if (!fill || !starts || !lens) return fail(SDFS_CDC_EINVAL, "null buffer");
+    Set& s = u.set();
+    const size_t i = Reg::pick(s, stream_key != SDFS_CDC_NO_STREAM, stream_key);
+    Reg::Load ld(s, i);
+    return dev_get_chunks(
+        s.devs[i].get(), len, [&](uint8_t* dst) { return fill(ctx, dst, len); }, starts, lens, digests, cap, count);
+}
+
+static int copy_fill(void* ctx, uint8_t* dst, uint32_t len) {
+    memcpy(dst, ctx, len);
+    return 0;
+}
+
+int sdfs_cdc_get_chunks_stream(sdfs_cdc_engine* e, uint64_t stream_key, const uint8_t* buf, uint32_t len,
+                               uint32_t* starts, uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count) {
+    if (len && !buf) return fail(SDFS_CDC_EINVAL, "null buffer");
+    return sdfs_cdc_get_chunks_fill(e, stream_key, len, copy_fill, const_cast<uint8_t*>(buf), starts, lens, digests,
+                                    cap, count);
+}
+
+int sdfs_cdc_get_chunks(sdfs_cdc_engine* e, const uint8_t* buf, uint32_t len, uint32_t* starts, uint32_t* lens,
+                        uint8_t* digests, uint32_t cap, uint32_t* count) {
+    return sdfs_cdc_get_chunks_stream(e, SDFS_CDC_NO_STREAM, buf, len, starts, lens, digests, cap, count);
+}
+
+int sdfs_cdc_get_hash(sdfs_cdc_engine* e, const uint8_t* data, uint64_t len, uint8_t* digest) {
+    if (!digest || (len && !data)) return fail(SDFS_CDC_EINVAL, "null argument");
+    if (len > 0xFFFFFFFFull) return fail(SDFS_CDC_EINVAL, "getHash input > 4 GiB");
+    USE_OR_FAIL(u, e);
+    Set& s = u.set();
+    const size_t i = Reg::pick(s, false, 0);
+    Reg::Load ld(s, i);
+    return dev_get_hash(s.devs[i].get(), data, len, digest);
+}
+
+int sdfs_cdc_queue_stats(sdfs_cdc_engine* e, uint64_t* batches, uint64_t* requests) {
+    USE_OR_FAIL(u, e);
+    uint64_t b = 0, r = 0;
+    for (auto& d : u.set().devs) {
+        std::lock_guard<std::mutex> lk(d->q_init);
+        if (d->q) {
+            b += d->q->batches();
+            r += d->q->requests();
+        }
+    }
+    if (batches) *batches = b;
+    if (requests) *requests = r;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_queue_timing(sdfs_cdc_engine* e, double* fill_us, double* copy_us, double* device_us) {
+    USE_OR_FAIL(u, e);
+    double f = 0, c = 0, dv = 0, wsum = 0;
+    for (auto& d : u.set().devs) {
+        std::lock_guard<std::mutex> lk(d->q_init);
+        if (!d->q) continue;
+        double a, b, x;
+        d->q->timing(&a, &b, &x);
+        const double w = (double)d->q->batches();
+        f += a * w;
+        c += b * w;
+        dv += x * w;
+        wsum += w;
+    }
+    if (wsum > 0) f /= wsum, c /= wsum, dv /= wsum;
+    if (fill_us) *fill_us = f;
+    if (copy_us) *copy_us = c;
+    if (device_us) *device_us = dv;
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_host_register(void* p, uint64_t n) {
+    if (!p || !n) return fail(SDFS_CDC_EINVAL, "null or empty region");
+    HIP_TRY(hipHostRegister(p, n, hipHostRegisterPortable));  // pinned for every device of a set
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_host_unregister(void* p) {
+    if (!p) return fail(SDFS_CDC_EINVAL, "null region");
+    HIP_TRY(hipHostUnregister(p));
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_hash_device(sdfs_cdc_engine* e, const uint8_t* d_data, const uint64_t* d_offs, const uint32_t* d_lens,
+                         const uint32_t* d_count, uint64_t n_max, uint8_t* d_digests, void* stream) {
+    USE_OR_FAIL(u, e);
+    if (n_max && (!d_data || !d_offs || !d_lens || !d_digests)) return fail(SDFS_CDC_EINVAL, "null argument");
+    size_t i = 0;
+    if (n_max) {
+        const int rc = dev_of_ptr(u.set(), d_data, &i);
+        if (rc) return rc;
+    }
+    DevEngine* d = u.set().devs[i].get();
+    std::lock_guard<std::mutex> lk(d->mu);
+    HIP_TRY(hipSetDevice(d->prm.device));
+    return hash_extents(d, d_data, d_offs, d_lens, d_count, n_max, d_digests, reinterpret_cast<hipStream_t>(stream));
+}
+
+int sdfs_cdc_get_hash_batch(sdfs_cdc_engine* e, const uint8_t* base, const uint64_t* offs, const uint32_t* lens,
+                            uint32_t n, uint8_t* digests) {
+    USE_OR_FAIL(u, e);
+    if (n == 0) return SDFS_CDC_OK;
+    if (!base || !offs || !lens || !digests) return fail(SDFS_CDC_EINVAL, "null argument");
+    Set& s = u.set();
+    const size_t i = Reg::pick(s, false, 0);
+    Reg::Load ld(s, i);
+    return dev_get_hash_batch(s.devs[i].get(), base, offs, lens, n, digests);
+}
+
 int sdfs_cdc_synth_device(sdfs_cdc_engine* e, uint8_t* d_out, uint64_t n, uint64_t seed, uint64_t stream,
                           uint64_t offset, void* stream_handle) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    HIP_TRY(hipSetDevice(e->prm.device));
+    USE_OR_FAIL(u, e);
+    size_t i;
+    const int rc = dev_of_ptr(u.set(), d_out, &i);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(u.set().ordinals[i]));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_handle);  // NULL = the HIP null stream
     HIP_TRY(launch_synth(d_out, n, seed, stream, offset, s));
     return SDFS_CDC_OK;
 }
 
 int sdfs_cdc_stream_sync(sdfs_cdc_engine* e) {
-    if (!e) return fail(SDFS_CDC_EINVAL, "null engine");
-    HIP_TRY(hipSetDevice(e->prm.device));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    USE_OR_FAIL(u, e);
+    for (auto& d : u.set().devs) {
+        HIP_TRY(hipSetDevice(d->prm.device));
+        HIP_TRY(hipStreamSynchronize(d->stream));
+    }
+    return SDFS_CDC_OK;
+}
+
+int sdfs_cdc_allgather_records(sdfs_cdc_engine* e, uint8_t* const* records, const uint64_t* records_cap,
+                               const uint32_t* const* d_totals, uint8_t* const* gathered, uint64_t gathered_cap,
+                               uint32_t* counts, uint64_t* stride, void* const* streams) {
+    USE_OR_FAIL(u, e);
+    if (!records || !records_cap || !d_totals || !gathered || !counts || !stride)
+        return fail(SDFS_CDC_EINVAL, "null argument");
+    Set& s = u.set();
+    const int n = (int)s.ndev();
+    for (int i = 0; i < n; i++)
+        if (!records[i] || !d_totals[i] || !gathered[i]) return fail(SDFS_CDC_EINVAL, "null table of device %d", i);
+    Coll* c = nullptr;
+    int rc = coll_ready(s, &c);
+    if (rc) return rc;
+    const RcclApi* api = rccl_api();
+    auto st = [&](int i) { return streams ? reinterpret_cast<hipStream_t>(streams[i]) : (hipStream_t) nullptr; };
+    std::lock_guard<std::mutex> lk(s.coll_mu);  // one exchange of the set at a time (shared count buffers)
+    // 1. counts: one u32 per device, gathered on every device; device 0's copy to the host
+    NCCL_TRY(api, api->group_start());
+    for (int i = 0; i < n; i++) {
+        HIP_TRY(hipSetDevice(s.ordinals[i]));
+        NCCL_TRY(api, api->all_gather(d_totals[i], c->d_counts[i], 1, kNcclUint32, c->comms[i], st(i)));
+    }
+    NCCL_TRY(api, api->group_end());
+    HIP_TRY(hipSetDevice(s.ordinals[0]));
+    HIP_TRY(hipMemcpyAsync(c->h_counts, c->d_counts[0], 4ull * n, hipMemcpyDeviceToHost, st(0)));
+    HIP_TRY(hipStreamSynchronize(st(0)));
+    uint64_t m = 0;
+    for (int i = 0; i < n; i++) {
+        counts[i] = c->h_counts[i];
+        m = std::max<uint64_t>(m, counts[i]);
+    }
+    for (int i = 0; i < n; i++)
+        if (records_cap[i] < m)
+            return fail(SDFS_CDC_ECAP, "device %d holds %llu records, the largest table has %llu", i,
+                        (unsigned long long)records_cap[i], (unsigned long long)m);
+    if ((uint64_t)n * m > gathered_cap)
+        return fail(SDFS_CDC_ECAP, "gathered table of %llu records > capacity %llu", (unsigned long long)((uint64_t)n * m),
+                    (unsigned long long)gathered_cap);
+    *stride = m;
+    if (m == 0) return SDFS_CDC_OK;
+    // 2. the tables, padded to the largest count: device j's records at gathered[i] + j*m*48
+    NCCL_TRY(api, api->group_start());
+    for (int i = 0; i < n; i++) {
+        HIP_TRY(hipSetDevice(s.ordinals[i]));
+        NCCL_TRY(api, api->all_gather(records[i], gathered[i], m * SDFS_CDC_RECORD_BYTES, kNcclUint8, c->comms[i],
+                                      st(i)));
+    }
+    NCCL_TRY(api, api->group_end());
     return SDFS_CDC_OK;
 }
 

@@ -216,13 +216,16 @@ class CoalescingQueue {
         max_req_ = c_.max_req_bytes ? c_.max_req_bytes : slots_[0].cap / 2;
         prepared_ = true;
         stop_ = false;
+        disp_done_ = false;
         disp_ = std::thread([this] { dispatcher(); });
         for (int l = 0; l < c_.lanes; l++) comp_.emplace_back([this, l] { completer(l); });
         return 0;
     }
 
-    // Stops the threads (after the in-flight batches completed) and releases the slots.  No
-    // request may be in progress.
+    // Stops the queue: callers that arrive from now on, and callers still waiting for room, get
+    // kQueueStopped; every request already placed in a slot is launched and completed (the open
+    // slot included), its caller reads its result; then the threads end and, once the last
+    // caller has left run(), the slots are released.
     void shutdown() {
         {
             std::lock_guard<std::mutex> lk(m_);
@@ -236,7 +239,8 @@ class CoalescingQueue {
         for (auto& t : comp_)
             if (t.joinable()) t.join();
         comp_.clear();
-        std::lock_guard<std::mutex> lk(m_);
+        std::unique_lock<std::mutex> lk(m_);
+        idle_cv_.wait(lk, [&] { return active_ == 0; });
         for (auto& s : slots_) b_.release(s);
         prepared_ = false;
     }
@@ -246,6 +250,21 @@ class CoalescingQueue {
     // caller's results out, or reports the batch's failure `status`; its return value is run's.
     template <class ReadFn>
     int run(QReq& r, ReadFn&& read) {
+        return run_fill(
+            r,
+            [&r](uint8_t* dst) {
+                if (r.len) memcpy(dst, r.src, r.len);
+                return 0;
+            },
+            read);
+    }
+
+    // The same, with the caller's bytes written into the slot's staging by `fill(dst)` (r.len
+    // bytes; a non-zero return is this call's result, its bytes still travel with the batch): a
+    // caller whose bytes are not in plain memory (a JNI byte[]) copies them once, straight into
+    // the pinned staging.
+    template <class FillFn, class ReadFn>
+    int run_fill(QReq& r, FillFn&& fill, ReadFn&& read) {
         std::unique_lock<std::mutex> lk(m_);
         if (!prepared_ || stop_) return kQueueStopped;
         if (r.len > max_req_) return kQueueTooBig;  // callers check accepts() first
@@ -266,30 +285,30 @@ class CoalescingQueue {
                         waitq_.erase(it);
                         break;
                     }
-                active_--;
+                leave();
                 return kQueueStopped;
             }
             rc = r.admit;
         }
         if (rc != 1) {  // not even an empty slot takes it
-            active_--;
+            leave();
             return kQueueTooBig;
         }
         QSlot* s = &slots_[r.slot];
         cv_disp_.notify_one();
         lk.unlock();
-        if (r.len) memcpy(s->in + r.off, r.src, r.len);
+        const int frc = fill(s->in + r.off);
         lk.lock();
         if (--s->copying == 0) cv_disp_.notify_all();
         done_cv_[r.slot].wait(lk, [&] { return r.done; });  // woken with its own slot only
         lk.unlock();
-        const int ret = read(*s, r, r.status);
+        const int ret = frc ? frc : read(*s, r, r.status);
         lk.lock();
-        active_--;
         if (--s->readers == 0) {
             s->state = QSlot::kFree;
             admit_waiting();
         }
+        leave();
         return ret;
     }
 
@@ -313,6 +332,11 @@ class CoalescingQueue {
     }
 
   private:
+    // a caller leaves run() (queue lock held)
+    void leave() {
+        if (--active_ == 0 && stop_) idle_cv_.notify_all();
+    }
+
     std::condition_variable& admit_cv(const QReq* q) {
         return cv_admit_[(reinterpret_cast<uintptr_t>(q) >> 6) % kAdmitCvs];
     }
@@ -375,6 +399,7 @@ class CoalescingQueue {
     // Room may have appeared (a slot launched or freed): place waiting requests in arrival order
     // while they fit and wake their callers (queue lock held).
     void admit_waiting() {
+        if (stop_) return;  // the waiting callers see stop_ and leave
         bool any = false;
         while (!waitq_.empty()) {
             QReq* q = waitq_.front();
@@ -394,6 +419,7 @@ class CoalescingQueue {
         const QSlot& o = slots_[open_];
         const size_t n = o.nreq();
         if (n == 0) return false;
+        if (stop_) return true;  // draining: launch what was placed
         const size_t share = (size_t)((active_ + c_.lanes - 1) / c_.lanes);
         if (inflight_ == 0 || o.full || n >= share) return true;
         *deadline = o.t_open + std::chrono::microseconds(c_.linger_us);
@@ -404,7 +430,8 @@ class CoalescingQueue {
         std::unique_lock<std::mutex> lk(m_);
         for (;;) {
             std::chrono::steady_clock::time_point deadline{};
-            while (!stop_ && !ready(&deadline)) {
+            while (!ready(&deadline)) {
+                if (stop_ && (open_ < 0 || slots_[open_].nreq() == 0)) break;  // nothing left to launch
                 if (deadline != std::chrono::steady_clock::time_point{}) {
                     // a timed wait on the system clock (pthread_cond_timedwait): the steady-clock
                     // form (pthread_cond_clockwait) is invisible to the GCC 11 ThreadSanitizer;
@@ -417,7 +444,7 @@ class CoalescingQueue {
                 }
                 deadline = {};
             }
-            if (stop_) break;
+            if (!ready(&deadline)) break;  // stopped with nothing placed
             QSlot& s = slots_[open_];
             s.state = QSlot::kClosed;
             s.t_close = std::chrono::steady_clock::now();
@@ -441,14 +468,16 @@ class CoalescingQueue {
             flight_[lane].push_back(&s);
             comp_cv_[lane].notify_one();
         }
+        disp_done_ = true;  // completers may end once nothing is in flight
+        for (auto& cv : comp_cv_) cv.notify_all();
     }
 
     // One per lane: a lane's batches complete in launch order (one stream).
     void completer(int lane) {
         std::unique_lock<std::mutex> lk(m_);
         for (;;) {
-            comp_cv_[lane].wait(lk, [&] { return !flight_[lane].empty() || (stop_ && inflight_ == 0); });
-            if (flight_[lane].empty()) break;  // stop_ and nothing in flight
+            comp_cv_[lane].wait(lk, [&] { return !flight_[lane].empty() || (disp_done_ && inflight_ == 0); });
+            if (flight_[lane].empty()) break;  // dispatcher gone and nothing in flight
             QSlot* s = flight_[lane].front();
             flight_[lane].pop_front();
             const int launched_rc = s->status;
@@ -474,7 +503,7 @@ class CoalescingQueue {
             }
             done_cv_[s - slots_.data()].notify_all();
             cv_disp_.notify_all();
-            if (stop_ && inflight_ == 0)
+            if (disp_done_ && inflight_ == 0)
                 for (auto& cv : comp_cv_) cv.notify_all();
         }
     }
@@ -498,8 +527,10 @@ class CoalescingQueue {
     int open_ = -1;
     int inflight_ = 0;
     int active_ = 0;  // callers inside run()
+    std::condition_variable idle_cv_;  // active_ reached 0 while stopping
     bool prepared_ = false;
     bool stop_ = false;
+    bool disp_done_ = false;  // the dispatcher has ended (stopping)
     uint64_t max_req_ = 0;
     uint64_t seq_ = 0;
     uint64_t launched_ = 0, served_ = 0, timed_ = 0;

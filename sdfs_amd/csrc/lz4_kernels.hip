@@ -986,8 +986,14 @@ __global__ __launch_bounds__(256) void lz4_lane_kernel(Lz4Args a) {
         const uint64_t c = a.idx ? a.idx[i] : i;  // longest-first order: a wave's lanes end together
         const uint32_t n = a.src_len[c];
         const uint8_t* src = a.data + a.src_off[c];
+        // A lane's table entries hold (generation << 17) | position: a chunk longer than 128 KiB
+        // would spill position bits into the generation field, so it goes to the wave kernel.
+        if (n > (1u << kLanePosBits)) {
+            a.bail[1 + atomicAdd(a.bail, 1u)] = (uint32_t)c;
+            continue;
+        }
         if constexpr (PT) {
-            if (a.bail) {
+            if (a.bail_misses) {
                 const uint32_t m = n < kPretestBytes ? n : kPretestBytes;
 #pragma unroll 8
                 for (uint32_t h = 0; h < 64; h++) pt[h * 256 + threadIdx.x] = 0;
@@ -1179,14 +1185,13 @@ int launch_compress_impl(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
             LZ_TRY(launch_extent_order(x, s));
             g.idx = x.tasks;
         }
-        if (hybrid) {
-            LZ_TRY(z->bail.ensure(a.n_max + 1));
-            LZ_TRY(hipMemsetAsync(z->bail.p, 0, 4, s));
-            g.bail = z->bail.p;
-            g.bail_misses = z->bail_misses;
-        }
+        // Both lane modes keep a bail list: chunks over 128 KiB always go to the wave kernel; the
+        // hybrid also bails on chunks that look incompressible (pre-test, then bail_misses misses).
+        LZ_TRY(z->bail.ensure(a.n_max + 1));
+        LZ_TRY(hipMemsetAsync(z->bail.p, 0, 4, s));
+        g.bail = z->bail.p;
+        g.bail_misses = hybrid ? z->bail_misses : 0u;
         LZ_TRY(launch_lane(z->mode, z->lane_depth, z->pretest != 0, (uint32_t)grid, g, s));
-        if (!hybrid) return SDFS_CDC_OK;
         Lz4Args w = a;  // the bailed chunks, one wave each
         w.d_count = z->bail.p;
         w.idx = z->bail.p + 1;

@@ -142,6 +142,23 @@ class SdfsConfig:
         return p
 
 
+def stream_key(uuid: str) -> int:
+    """Stream key of a write stream's uuid (the file GUID getChunks is called with,
+    SparseDedupFile.java:432): Java's String.hashCode as an unsigned 32-bit value, which is what
+    the JNI glue passes."""
+    b = uuid.encode("utf-16-le")
+    h = 0
+    for i in range(0, len(b), 2):
+        h = (31 * h + int.from_bytes(b[i:i + 2], "little")) & 0xFFFFFFFF
+    return h
+
+
+def check_count(rc: int) -> int:
+    if rc < 0:
+        check(rc)
+    return rc
+
+
 def _buf(data) -> tuple[np.ndarray, int]:
     a = np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) else np.asarray(data)
     a = np.ascontiguousarray(a, np.uint8)
@@ -154,11 +171,15 @@ class HipVariableSha256HashEngine:
     HASH256 = "HASH256"
     HASH160 = "HASH160"
 
-    def __init__(self, ht: str = HASH256, config: SdfsConfig | None = None, device: int = 0):
+    def __init__(self, ht: str = HASH256, config: SdfsConfig | None = None, device: int = 0, device_mask: int = 0):
+        """device: HIP ordinal, or -1 (ALL_DEVICES) for a device set of every gfx950 GPU;
+        device_mask: bit i = ordinal i in the set (overrides device).  Engines with equal
+        parameters and device sets share one native engine (include/sdfs_cdc.h "Sharing")."""
         self.config = config or SdfsConfig()
         self.ht = ht
         hash_type = VARIABLE_SHA256_160 if ht == self.HASH160 else self._hash_type()
         self._params = self.config.to_params(device=device, hash_type=hash_type)
+        self._params.device_mask = device_mask
         self._lib = _lib.load()
         h = ctypes.c_void_p()
         check(self._lib.sdfs_cdc_create(ctypes.byref(self._params), ctypes.byref(h)))
@@ -221,9 +242,10 @@ class HipVariableSha256HashEngine:
 
     def getChunks(self, data: bytes, uuid: str | None = None) -> list[Finger]:
         """VariableSha256HashEngine.getChunks (:71-86): fresh CDC state per call; returns the
-        ordered, contiguous Finger list covering the buffer, each with a copy of its bytes."""
+        ordered, contiguous Finger list covering the buffer, each with a copy of its bytes.  The
+        uuid names the write stream: on a device set its buffers stay on one GPU."""
         a, ptr = _buf(data)
-        starts, lens, digs = self.chunk_arrays(a)
+        starts, lens, digs = self.chunk_arrays(a, stream_key=None if uuid is None else stream_key(uuid))
         raw = a.tobytes()
         return [Finger(uuid, raw[s: s + n], digs[i].tobytes(), int(s), int(n))
                 for i, (s, n) in enumerate(zip(starts.tolist(), lens.tolist()))]
@@ -232,18 +254,46 @@ class HipVariableSha256HashEngine:
     def slot_cap(self, buf_len: int) -> int:
         return int(self._lib.sdfs_cdc_slot_cap(self._h, buf_len))
 
-    def chunk_arrays(self, data) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
-        """One buffer -> (starts u32[n], lens u32[n], digests u8[n, digest_len])."""
+    def chunk_arrays(self, data, stream_key: int | None = None,
+                     fill: bool = False) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """One buffer -> (starts u32[n], lens u32[n], digests u8[n, digest_len]).
+        stream_key: the write stream the buffer belongs to (sdfs_cdc_get_chunks_stream: a device
+        set keeps one stream on one GPU); fill: hand the bytes over through the fill callback
+        (sdfs_cdc_get_chunks_fill, the JNI glue's entry point) instead of a pointer."""
         a, ptr = _buf(data)
         cap = self.slot_cap(max(len(a), 1))
         st = np.zeros(cap, np.uint32)
         ln = np.zeros(cap, np.uint32)
         dg = np.zeros((cap, self.digest_len), np.uint8)
         n = ctypes.c_uint32()
-        check(self._lib.sdfs_cdc_get_chunks(self._h, ptr, len(a), st.ctypes.data, ln.ctypes.data, dg.ctypes.data,
-                                            cap, ctypes.byref(n)))
+        key = _lib.NO_STREAM if stream_key is None else int(stream_key) & _lib.NO_STREAM
+        if fill:
+            def _fill(ctx, dst, ln_):
+                ctypes.memmove(dst, ptr, ln_)
+                return 0
+
+            cb = _lib.FILL_FN(_fill)
+            check(self._lib.sdfs_cdc_get_chunks_fill(self._h, key, len(a), cb, None, st.ctypes.data, ln.ctypes.data,
+                                                     dg.ctypes.data, cap, ctypes.byref(n)))
+        elif stream_key is None:
+            check(self._lib.sdfs_cdc_get_chunks(self._h, ptr, len(a), st.ctypes.data, ln.ctypes.data, dg.ctypes.data,
+                                                cap, ctypes.byref(n)))
+        else:
+            check(self._lib.sdfs_cdc_get_chunks_stream(self._h, key, ptr, len(a), st.ctypes.data, ln.ctypes.data,
+                                                       dg.ctypes.data, cap, ctypes.byref(n)))
         k = n.value
         return st[:k].copy(), ln[:k].copy(), dg[:k].copy()
+
+    # ---- device set and sharing ----
+    def device_count(self) -> int:
+        return check_count(self._lib.sdfs_cdc_device_count(self._h))
+
+    def device_ordinals(self) -> list[int]:
+        return [check_count(self._lib.sdfs_cdc_device_ordinal(self._h, i)) for i in range(self.device_count())]
+
+    def share_count(self) -> int:
+        """Live engine handles sharing this one's native engine (1 = not shared)."""
+        return check_count(self._lib.sdfs_cdc_share_count(self._h))
 
     def chunk_batch(self, base, offs, lens):
         """Many independent buffers (base[offs[b] : offs[b]+lens[b]]) in one GPU pass.
@@ -304,11 +354,29 @@ class HipVariableSha256HashEngine:
             mask |= 1 << self.STAGES.index(s)
         check(self._lib.sdfs_cdc_set_timing_mask(self._h, int(nruns), mask))
 
-    def kernel_times(self) -> dict[str, float]:
+    def kernel_times(self, dev_index: int = 0) -> dict[str, float]:
         names = (ctypes.c_char_p * 8)()
         ms = (ctypes.c_float * 8)()
-        n = self._lib.sdfs_cdc_kernel_times(self._h, names, ms, 8)
+        n = self._lib.sdfs_cdc_kernel_times_on(self._h, int(dev_index), names, ms, 8)
+        if n < 0:
+            check(n)
         return {names[i].decode(): float(ms[i]) for i in range(max(n, 0))}
+
+    def allgather_records(self, records, totals, gathered, streams=None):
+        """In-process RCCL all-gather of the device set's fingerprint tables (one entry per set
+        member, set order): records[i] u8 [cap_i, 48] and totals[i] (int32/uint32 [1]) on device
+        i, gathered[i] u8 [>= n*stride, 48] on device i.  Returns (counts list, stride)."""
+        n = len(records)
+        rp = (ctypes.c_void_p * n)(*[r.data_ptr() for r in records])
+        caps = (ctypes.c_uint64 * n)(*[int(r.numel() // 48) for r in records])
+        tp = (ctypes.c_void_p * n)(*[t.data_ptr() for t in totals])
+        gp = (ctypes.c_void_p * n)(*[g.data_ptr() for g in gathered])
+        gcap = min(int(g.numel() // 48) for g in gathered)
+        counts = (ctypes.c_uint32 * n)()
+        stride = ctypes.c_uint64()
+        sp = (ctypes.c_void_p * n)(*streams) if streams is not None else None
+        check(self._lib.sdfs_cdc_allgather_records(self._h, rp, caps, tp, gp, gcap, counts, ctypes.byref(stride), sp))
+        return list(counts), int(stride.value)
 
     def __del__(self):
         try:

@@ -50,10 +50,11 @@ def test_python_binding_covers_header():
 
 
 def test_struct_layouts_match_header():
-    # sdfs_cdc_params: 8+4+4+4+4+8+8+4+4+4+4+8 = 64 bytes; sdfs_cdc_dev_out: 4 ptrs + 2 u32 + ptr + u64 + ptr
-    assert ctypes.sizeof(_lib.Params) == 64
+    # sdfs_cdc_params: 8+4+4+4+4+8+8+4+4+4+4+8+8 = 72 bytes (ABI 2 added device_mask);
+    # sdfs_cdc_dev_out: 4 ptrs + 2 u32 + ptr + u64 + ptr
+    assert ctypes.sizeof(_lib.Params) == 72
     assert ctypes.sizeof(_lib.DevOut) == 64
-    assert _lib.load().sdfs_cdc_abi_version() == 1
+    assert _lib.load().sdfs_cdc_abi_version() == 2
 
 
 def test_default_params_are_the_reference_defaults():
@@ -81,12 +82,30 @@ def test_no_device_fails_loudly():
 
 def test_invalid_params_rejected_before_device():
     lib = _lib.load()
-    for field, val in [("window", 47), ("poly", 0x1FF), ("max_len", 0), ("hash_algo", 9), ("min_cmp", 5)]:
+    for field, val in [("window", 47), ("poly", 0x1FF), ("max_len", 0), ("hash_algo", 9), ("min_cmp", 5),
+                       ("device", -7)]:
         p = _lib.default_params()
         setattr(p, field, val)
         h = ctypes.c_void_p()
         assert lib.sdfs_cdc_create(ctypes.byref(p), ctypes.byref(h)) == _lib.EINVAL, field
         assert lib.sdfs_cdc_last_error()
+
+
+def test_handles_refused_after_destroy_and_unknown():
+    """Every handle-taking call on a pointer that is not a live handle fails with EINVAL (no
+    use of freed memory), with or without a device."""
+    lib = _lib.load()
+    bogus = ctypes.c_void_p(0x1234567)
+    assert lib.sdfs_cdc_destroy(bogus) == _lib.EINVAL
+    assert lib.sdfs_cdc_device_count(bogus) == _lib.EINVAL
+    assert lib.sdfs_cdc_share_count(bogus) == _lib.EINVAL
+    assert lib.sdfs_cdc_get_max_len(bogus) == -1
+    assert lib.sdfs_cdc_slot_cap(bogus, 262144) == 0
+    n = ctypes.c_uint32()
+    buf = (ctypes.c_uint8 * 64)()
+    out = (ctypes.c_uint32 * 8)()
+    assert lib.sdfs_cdc_get_chunks(bogus, buf, 64, out, out, None, 8, ctypes.byref(n)) == _lib.EINVAL
+    assert lib.sdfs_cdc_destroy(None) == _lib.OK
 
 
 def test_product_package_never_touches_the_oracle():

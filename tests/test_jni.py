@@ -46,7 +46,7 @@ class Jni:
         for n in ("nativeSlotCap",):
             getattr(g, PFX + n).argtypes = [VP, VP, ctypes.c_int64, ctypes.c_int32]
         getattr(g, PFX + "nativeDigestLen").argtypes = [VP, VP, ctypes.c_int64]
-        getattr(g, PFX + "nativeGetChunks").argtypes = [VP, VP, ctypes.c_int64, VP, VP, VP, VP]
+        getattr(g, PFX + "nativeGetChunks").argtypes = [VP, VP, ctypes.c_int64, VP, ctypes.c_int64, VP, VP, VP]
         getattr(g, PFX + "nativeGetHash").argtypes = [VP, VP, ctypes.c_int64, VP, VP]
         getattr(g, PFX + "nativeRegister").argtypes = [VP, VP, VP]
         self.env = s.stub_env()
@@ -107,7 +107,8 @@ def test_jni_get_chunks_and_get_hash_vs_oracle(algo):
         cap = j.call("nativeSlotCap", h, n)
         arr = j.byte_array(data)
         st, ln, dg = j.new(2, cap), j.new(2, cap), j.new(1, cap * dl)
-        cnt = j.call("nativeGetChunks", h, arr, st, ln, dg)
+        key = -1 if n % 2 else 0x9E3779B9  # no stream / a uuid's hashCode (unsigned)
+        cnt = j.call("nativeGetChunks", h, arr, key, st, ln, dg)
         assert j.exception() is None
         es, el, ed = O.chunk(data, prm)
         assert cnt == len(es)
@@ -124,7 +125,19 @@ def test_jni_get_chunks_and_get_hash_vs_oracle(algo):
     data = O.synth(O.SYNTH_SEED, 77, 0, 262144).tobytes()
     arr = j.byte_array(data)
     st, ln, dg = j.new(2, 2), j.new(2, 2), j.new(1, 2 * dl)
-    assert j.call("nativeGetChunks", h, arr, st, ln, dg) == -1
+    assert j.call("nativeGetChunks", h, arr, -1, st, ln, dg) == -1
     cls, msg = j.exception()
     assert cls == "java/io/IOException" and "cap" in msg
+    # a second Java instance with the same parameters shares the native engine (one queue)
+    from sdfs_amd import _lib
+    lib = _lib.load()
+    h2 = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, algo, 0)
+    assert h2 and h2 != h and j.exception() is None
+    assert lib.sdfs_cdc_share_count(ctypes.c_void_p(h)) == 2 == lib.sdfs_cdc_share_count(ctypes.c_void_p(h2))
     j.call("nativeDestroy", h)
+    assert lib.sdfs_cdc_share_count(ctypes.c_void_p(h2)) == 1
+    # the destroyed handle is refused (EINVAL: no use after free); the other still works
+    assert lib.sdfs_cdc_share_count(ctypes.c_void_p(h)) == _lib.EINVAL
+    st, ln, dg = j.new(2, 66), j.new(2, 66), j.new(1, 66 * dl)
+    assert j.call("nativeGetChunks", h2, arr, 7, st, ln, dg) == len(O.chunk(data, prm)[0])
+    j.call("nativeDestroy", h2)

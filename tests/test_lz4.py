@@ -284,6 +284,40 @@ def test_gpu_decompress_device_framed_records():
 
 
 @pytest.mark.gpu
+def test_gpu_hybrid_batch_with_records_over_128k_vs_oracle():
+    """A hybrid-size batch (>= 192 chunks per CU, so lanes compress the compressible chunks) that
+    also holds compressible records of 128 KiB + 1 .. 1 MiB: a lane's table entry keeps positions
+    in 17 bits, so those must go to the wave kernel; every record equals the oracle's."""
+    torch = pytest.importorskip("torch")
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    n_small = 192 * ncu + 64
+    rng = np.random.default_rng(128)
+    src = Z.text_like(1, 91, 8 << 20)
+    longs = [131072, 131073, 200000, 262144, 524288 + 17, 1 << 20]
+    lens = [int(x) for x in rng.integers(600, 2600, n_small)]
+    where = sorted(int(x) for x in rng.choice(n_small, len(longs), replace=False))
+    for w, n in zip(where, longs):
+        lens[w] = n
+    lens = np.array(lens, np.uint32)
+    # text windows (compressible: the lane path takes them unless they are too long); one long
+    # record is mostly zeros (long match runs)
+    starts = rng.integers(0, len(src) - (1 << 20) - 1, len(lens))
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 5)]).astype(np.uint64)
+    base = np.zeros(int(offs[-1]) + int(lens[-1]) + 16, np.uint8)
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        base[int(o): int(o) + int(n)] = src[int(starts[i]): int(starts[i]) + int(n)]
+    zo = int(offs[where[3]])
+    base[zo + 1000: zo + 250000] = 0
+    for mode in (Z.R123, Z.V19):
+        got = comp(mode).compress_chunks(base, offs, lens, framed=True)
+        want, _ = Z.compress_batch(base, offs, lens, mode, 16)
+        for i in where:
+            assert got[i] == want[i], (mode, int(lens[i]))
+        bad = [i for i in range(len(lens)) if got[i] != want[i]]
+        assert not bad, (mode, len(bad), bad[:8])
+
+
+@pytest.mark.gpu
 def test_gpu_large_batch_hybrid_vs_oracle():
     """A batch large enough for the product library's hybrid (one lane per chunk, bailed
     incompressible chunks re-run one wave each: >= 192 chunks per CU): every record of a

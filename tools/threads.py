@@ -34,15 +34,25 @@ def load():
         vp = ctypes.c_void_p
         lib.sdfs_threads_getchunks.argtypes = [vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                                ctypes.c_uint32, vp, vp, vp, vp, ctypes.POINTER(Result)]
+        lib.sdfs_threads_getchunks_ex.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint64,
+                                                  ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, vp, vp, vp, vp,
+                                                  ctypes.POINTER(Result)]
         lib.sdfs_threads_gethash.argtypes = [vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                              ctypes.c_int, vp, ctypes.POINTER(Result)]
         _lib = lib
     return _lib
 
 
-def getchunks(engine, nthreads: int, data: np.ndarray, buf_len: int, total_calls: int, keep: bool = False):
+MODES = {"copy": 0, "fill": 1, "stream": 2}
+
+
+def getchunks(engine, nthreads: int, data: np.ndarray, buf_len: int, total_calls: int, keep: bool = False,
+              engines=None, mode: str = "copy"):
     """data: nbuf * buf_len host bytes.  Returns (Result, results) where results is
-    (counts[nbuf], starts[nbuf, cap], lens[nbuf, cap], digests[nbuf, cap, dl]) when keep."""
+    (counts[nbuf], starts[nbuf, cap], lens[nbuf, cap], digests[nbuf, cap, dl]) when keep.
+    engines: several engine instances (thread t calls through engines[t % len]); mode: the
+    getChunks entry point ("copy" sdfs_cdc_get_chunks, "fill" the JNI glue's
+    sdfs_cdc_get_chunks_fill, "stream" sdfs_cdc_get_chunks_stream keyed by buffer // 16)."""
     lib = load()
     data = np.ascontiguousarray(data, np.uint8)
     nbuf = data.size // buf_len
@@ -56,8 +66,10 @@ def getchunks(engine, nthreads: int, data: np.ndarray, buf_len: int, total_calls
         ptrs = (counts.ctypes.data, st.ctypes.data, ln.ctypes.data, dg.ctypes.data)
     else:
         ptrs = (None, None, None, None)
-    rc = lib.sdfs_threads_getchunks(engine._h, nthreads, data.ctypes.data, nbuf, buf_len, total_calls, cap, *ptrs,
-                                    ctypes.byref(res))
+    hs = engines or [engine]
+    harr = (ctypes.c_void_p * len(hs))(*[h._h.value for h in hs])
+    rc = lib.sdfs_threads_getchunks_ex(harr, len(hs), MODES[mode], nthreads, data.ctypes.data, nbuf, buf_len,
+                                       total_calls, cap, *ptrs, ctypes.byref(res))
     if rc:
         raise RuntimeError(f"threads harness failed to start its threads ({rc})")
     return res, ((counts, st, ln, dg) if keep else None)

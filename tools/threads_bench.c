@@ -28,6 +28,9 @@ typedef struct sdfs_threads_result {
 typedef struct {
     sdfs_cdc_engine* e;
     int kind; /* 0 = getChunks, 1 = getHash */
+    int mode; /* getChunks: 0 = sdfs_cdc_get_chunks, 1 = sdfs_cdc_get_chunks_fill (the JNI glue's
+                 entry: the bytes are copied once, by the fill callback, into pinned staging),
+                 2 = sdfs_cdc_get_chunks_stream with stream key = buffer index / 16 */
     const uint8_t* data;
     uint64_t nbuf;
     uint32_t buf_len;
@@ -61,6 +64,11 @@ static double ts_us(const struct timespec* a, const struct timespec* b) {
     return (double)(b->tv_sec - a->tv_sec) * 1e6 + (double)(b->tv_nsec - a->tv_nsec) / 1e3;
 }
 
+static int copy_fill(void* ctx, uint8_t* dst, uint32_t len) {
+    memcpy(dst, ctx, len);
+    return 0;
+}
+
 static void* worker(void* arg) {
     worker_t* w = (worker_t*)arg;
     const int dl = sdfs_cdc_digest_len(w->e);
@@ -79,7 +87,13 @@ static void* worker(void* arg) {
             uint32_t* so = w->counts ? w->starts + b * w->cap : st;
             uint32_t* lo = w->counts ? w->lens + b * w->cap : ln;
             uint8_t* dgo = w->counts ? w->digests + b * w->cap * (uint64_t)dl : dg;
-            rc = sdfs_cdc_get_chunks(w->e, buf, w->buf_len, so, lo, dgo, w->cap, &n);
+            if (w->mode == 1)
+                rc = sdfs_cdc_get_chunks_fill(w->e, SDFS_CDC_NO_STREAM, w->buf_len, copy_fill, (void*)buf, so, lo, dgo,
+                                              w->cap, &n);
+            else if (w->mode == 2)
+                rc = sdfs_cdc_get_chunks_stream(w->e, b / 16, buf, w->buf_len, so, lo, dgo, w->cap, &n);
+            else
+                rc = sdfs_cdc_get_chunks(w->e, buf, w->buf_len, so, lo, dgo, w->cap, &n);
             if (w->counts && rc == 0) w->counts[b] = n;
         } else {
             rc = sdfs_cdc_get_hash(w->e, buf, w->buf_len, w->counts ? w->digests + b * 32 : dg);
@@ -100,10 +114,10 @@ static int cmp_d(const void* a, const void* b) {
     return x < y ? -1 : (x > y);
 }
 
-static int run(sdfs_cdc_engine* e, int kind, int nthreads, const uint8_t* data, uint64_t nbuf, uint32_t buf_len,
-               uint64_t total_calls, uint32_t cap, uint32_t* counts, uint32_t* starts, uint32_t* lens,
-               uint8_t* digests, sdfs_threads_result* res) {
-    if (!e || !data || nthreads < 1 || nbuf == 0 || !res || total_calls == 0) return -1;
+static int run(sdfs_cdc_engine* const* hs, int nh, int kind, int mode, int nthreads, const uint8_t* data, uint64_t nbuf,
+               uint32_t buf_len, uint64_t total_calls, uint32_t cap, uint32_t* counts, uint32_t* starts,
+               uint32_t* lens, uint8_t* digests, sdfs_threads_result* res) {
+    if (!hs || nh < 1 || !data || nthreads < 1 || nbuf == 0 || !res || total_calls == 0) return -1;
     worker_t* ws = calloc((size_t)nthreads, sizeof(worker_t));
     pthread_t* th = calloc((size_t)nthreads, sizeof(pthread_t));
     double* lat = calloc(total_calls, sizeof(double));
@@ -111,8 +125,9 @@ static int run(sdfs_cdc_engine* e, int kind, int nthreads, const uint8_t* data, 
     int started = 0;
     for (int t = 0; t < nthreads; t++) {
         worker_t* w = &ws[t];
-        w->e = e;
+        w->e = hs[t % nh]; /* thread t uses engine handle t mod nh (SDFS: many engine instances) */
         w->kind = kind;
+        w->mode = mode;
         w->data = data;
         w->nbuf = nbuf;
         w->buf_len = buf_len;
@@ -179,7 +194,17 @@ int sdfs_threads_getchunks(sdfs_cdc_engine* e, int nthreads, const uint8_t* data
                            uint64_t total_calls, uint32_t cap, uint32_t* counts, uint32_t* starts, uint32_t* lens,
                            uint8_t* digests, sdfs_threads_result* res) {
     if (res) memset(res, 0, sizeof(*res));
-    return run(e, 0, nthreads, data, nbuf, buf_len, total_calls, cap, counts, starts, lens, digests, res);
+    return run(&e, 1, 0, 0, nthreads, data, nbuf, buf_len, total_calls, cap, counts, starts, lens, digests, res);
+}
+
+/* The same over nh engine handles (thread t calls through handles[t % nh]) and an entry point
+ * (mode: 0 get_chunks, 1 get_chunks_fill, 2 get_chunks_stream). */
+int sdfs_threads_getchunks_ex(sdfs_cdc_engine* const* handles, int nh, int mode, int nthreads, const uint8_t* data,
+                              uint64_t nbuf, uint32_t buf_len, uint64_t total_calls, uint32_t cap, uint32_t* counts,
+                              uint32_t* starts, uint32_t* lens, uint8_t* digests, sdfs_threads_result* res) {
+    if (res) memset(res, 0, sizeof(*res));
+    return run(handles, nh, 0, mode, nthreads, data, nbuf, buf_len, total_calls, cap, counts, starts, lens, digests,
+               res);
 }
 
 /* T threads x getHash over the same buffers (digests[b * 32] kept when keep != 0). */
@@ -187,5 +212,6 @@ int sdfs_threads_gethash(sdfs_cdc_engine* e, int nthreads, const uint8_t* data, 
                          uint64_t total_calls, int keep, uint8_t* digests, sdfs_threads_result* res) {
     static uint32_t dummy;
     if (res) memset(res, 0, sizeof(*res));
-    return run(e, 1, nthreads, data, nbuf, buf_len, total_calls, 1, keep ? &dummy : NULL, NULL, NULL, digests, res);
+    return run(&e, 1, 1, 0, nthreads, data, nbuf, buf_len, total_calls, 1, keep ? &dummy : NULL, NULL, NULL, digests,
+               res);
 }
