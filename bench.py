@@ -3,11 +3,21 @@
 
 Workload (BASELINE.json configs[1]): per GPU, 64 independent synthetic write
 streams x 64 MiB, cut into CHUNK_LENGTH = 256 KiB write buffers (16384 buffers, 4 GiB) resident in
-HBM before the timed region; every buffer is chunked from a fresh CDC state with the reference
-parameters (P = 0x26CE86126EF863, W = 48, minLen 4095, maxLen 32768, 12-bit predicate, SHA-256).
+HBM before the timed region; every buffer is chunked from a fresh CDC state.  The headline uses
+the metric's chunk mix, a 4 KiB mean: min-variable-segment-size = 2 (minLen 2047,
+Config.java:145-148) and an 11-bit boundary predicate, with the reference's other parameters
+(P = 0x26CE86126EF863, W = 48, maxLen 32768, SHA-256); the reference-default mix (minLen 4095,
+12-bit predicate, ~8 KiB mean) is reported beside it (`at_ref_default`).
 One step = scan + cut resolution + SHA-256 of every chunk of the 4 GiB; at N > 1 the step also
-all-gathers the fingerprint table (48-byte records) over RCCL (sdfs_amd/dist.py).  Weak scaling:
-rank r owns streams [64r, 64r+64).
+all-gathers the fingerprint table (48-byte records) over RCCL.  Weak scaling: GPU r owns streams
+[64r, 64r+64).
+
+N > 1 runs two ways, the same work either way:
+* under a launcher (torch.distributed.run, the driver's form): one process per GPU, WORLD_SIZE
+  must equal --gpus, the exchange over torch.distributed "nccl" (RCCL; sdfs_amd/dist.py);
+* without one: ONE process drives all N GPUs through one engine whose device set is GPUs 0..N-1
+  (include/sdfs_cdc.h "Devices"), and the engine all-gathers the tables itself over RCCL
+  (sdfs_cdc_allgather_records, pipelined one step behind production).
 
 Production device path: one engine, steps alternating between two HIP streams (the engine's
 workspace ring keeps two batches in flight, so one batch's scan fills the tail of the other's
@@ -83,7 +93,8 @@ def load_traffic(name: str, params: str):
         d = json.load(open(path))
     except Exception:
         return None, None
-    if d.get("params") != params or name not in d:
+    d = d.get("by_params", {}).get(params) or (d if d.get("params") == params else None)
+    if not d or name not in d:
         return None, None
     return d[name].get("hbm_bytes_per_launch"), f"{d.get('source', '?')} (commit {d.get('commit', '?')})"
 
@@ -156,21 +167,23 @@ def timed(torch, dist, world, fn, steps):
     return el
 
 
-def threads_sweep(eng_cfg, device, host, buf_len, thread_counts):
+def threads_sweep(eng_cfg, device, host, buf_len, thread_counts, mode="fill"):
     """SDFS's own calling pattern: T C threads, each calling getChunks on one 256 KiB buffer at a
-    time through the C-ABI (coalesced into shared GPU passes); rate and per-call latency."""
+    time through the C-ABI (coalesced into shared GPU passes); rate and per-call latency.  mode
+    "fill" is the JNI glue's entry point (sdfs_cdc_get_chunks_fill: the byte[] copied once,
+    straight into the engine's pinned staging)."""
     from sdfs_amd import HashFunctionPool
     from tools import threads as T
 
-    out = {}
+    out = {"entry": "sdfs_cdc_get_chunks_fill (JNI glue)" if mode == "fill" else "sdfs_cdc_get_chunks"}
     eng = HashFunctionPool(eng_cfg, device=device).getHashEngine()
     # warm at the highest concurrency of the sweep, so every slot and lane has carried a pass
     tmax = max(thread_counts) if thread_counts else 8
-    T.getchunks(eng, tmax, host, buf_len, max(256, 4 * tmax))
+    T.getchunks(eng, tmax, host, buf_len, max(256, 4 * tmax), mode=mode)
     start = eng.queue_stats()
     for th in thread_counts:
         calls = max(256, th * 8)
-        r, _ = T.getchunks(eng, th, host, buf_len, calls)
+        r, _ = T.getchunks(eng, th, host, buf_len, calls, mode=mode)
         b0 = eng.queue_stats()
         out[str(th)] = {"gibps": round(r.gibps, 3), "p50_us": round(r.p50_us, 1), "p99_us": round(r.p99_us, 1),
                         "mean_us": round(r.mean_us, 1), "calls": r.calls, "errors": r.first_error}
@@ -185,6 +198,122 @@ def threads_sweep(eng_cfg, device, host, buf_len, thread_counts):
     eng.destroy()
     return out
 
+def main_device_set(args):
+    """--gpus N > 1 without a launcher: ONE process, one engine whose device set is GPUs 0..N-1.
+    GPU d owns streams [64d, 64d+64) (weak scaling, as one rank per GPU would), each GPU keeps two
+    batches in flight on two streams, and the engine all-gathers the record tables in process over
+    RCCL one step behind production (sdfs_amd/dist.py DeviceSetExchange)."""
+    import torch
+
+    from sdfs_amd import HipVariableSha256HashEngine, SdfsConfig
+    from sdfs_amd.device import DeviceBatch
+    from sdfs_amd.dist import DeviceSetExchange, shard_streams
+
+    n = args.gpus
+    if torch.cuda.device_count() < n:
+        log(f"bench.py: --gpus {n} but only {torch.cuda.device_count()} GPUs are visible")
+        sys.exit(2)
+    cfg = SdfsConfig(chunk_length=args.buf_kib * 1024, min_len=args.min_seg_kib * 1024 - 1,
+                     pred_mask=(1 << args.mask_bits) - 1, hash_type=args.hash_type)
+    eng = HipVariableSha256HashEngine(config=cfg, device=-1, device_mask=(1 << n) - 1)
+    assert eng.device_ordinals() == list(range(n))
+    buf_len = args.buf_kib * 1024
+    bufs_per_stream = args.stream_mib * 1024 // args.buf_kib
+    batches, streams = [], []
+    for d in range(n):
+        dev = f"cuda:{d}"
+        with torch.cuda.device(d):
+            sh = shard_streams(args.streams * n, n, d)
+            nbuf = len(sh) * bufs_per_stream
+            b0 = DeviceBatch(eng, nbuf=nbuf, buf_len=buf_len, device=dev)
+            b0.fill_streams(first_stream=sh.start, bufs_per_stream=bufs_per_stream)
+            b1 = DeviceBatch(eng, nbuf=nbuf, buf_len=buf_len, device=dev)
+            b1.data = b0.data
+            batches.append([b0, b1])
+            streams.append([torch.cuda.Stream(device=d), torch.cuda.Stream(device=d)])
+    for d in range(n):
+        torch.cuda.synchronize(d)
+    nbytes = batches[0][0].nbytes
+    cap_rec = batches[0][0].nbuf * batches[0][0].cap
+    ex = DeviceSetExchange(eng, cap_rec, [f"cuda:{d}" for d in range(n)])
+
+    def step(i):
+        for d in range(n):
+            b, s = batches[d][i % 2], streams[d][i % 2]
+            b.set_records(ex.acquire(i, d, s))
+            b.run(buffer_id_base=d * b.nbuf, stream=s.cuda_stream)
+            ex.produced(i, d, b.total, s)
+        if i >= 1:
+            ex.exchange(i - 1)
+
+    def sync_all():
+        for d in range(n):
+            torch.cuda.synchronize(d)
+
+    t_ramp = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t_ramp < args.ramp_secs:
+        step(i)
+        i += 1
+    for _ in range(args.warmup):
+        step(i)
+        i += 1
+    if i:
+        ex.exchange(i - 1)
+    sync_all()
+    eng.set_timing_stages(args.steps, ("chunk_hash",))
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(i + k)
+    ex.exchange(i + args.steps - 1)
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    hash_ms = [eng.kernel_times(d).get("chunk_hash", 0.0) for d in range(n)]
+    eng.set_timing(0)
+    totals = [int(batches[d][0].total.item()) for d in range(n)]
+    counts, stride = ex.results[-1]
+    value = n * nbytes * args.steps / elapsed / 2**30
+    ms_step = elapsed / args.steps * 1e3
+    t_dom = hash_ms[0] / 1e3
+    achieved = nbytes / t_dom / 1e9 if t_dom > 0 else 0.0
+    params = (f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
+              f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen {args.hash_type}")
+    traffic, traffic_src = load_traffic("chunk_hash", params)
+    res = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (counter-based SplitMix64 streams, 0% duplicate), resident in HBM",
+        "config": {
+            "workload": f"{args.streams} streams x {args.stream_mib} MiB per GPU, CHUNK_LENGTH {buf_len} B "
+                        f"({batches[0][0].nbuf} buffers, {nbytes / 2**30:.2f} GiB per GPU), fresh CDC state per buffer",
+            "params": params,
+            "mean_chunk_bytes": round(n * nbytes / max(sum(totals), 1), 1),
+            "chunks_per_gpu_step": totals,
+            "streams_in_flight": 2,
+            "exchange": "in-process RCCL all-gather of the 48-B fingerprint records by the engine "
+                        "(sdfs_cdc_allgather_records), pipelined one step behind production",
+            "exchange_last_step": {"counts": counts, "stride": stride},
+            "parallelism": f"device set of {n} GPUs in one process (streams sharded per GPU)",
+        },
+        "kernels_ms": {"chunk_hash_per_gpu": [round(x, 4) for x in hash_ms]},
+        "roofline": {"bound": "hbm", "kernel": "chunk_hash", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src},
+        "cpu_baseline": None,
+        "commit": git_head(),
+    }
+    print(json.dumps(res), flush=True)
+    eng.destroy()
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -198,13 +327,19 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-1t-secs", type=float, default=3.0, help="single-thread CPU baseline sample (0 = skip)")
     ap.add_argument("--e2e-mib", type=int, default=1024, help="host->GPU->host batch measurement size (0 = skip)")
-    ap.add_argument("--threads", default="1,8,32,64,128,256",
-                    help="getChunks caller-thread counts for the coalescing-queue sweep ('' = skip)")
-    ap.add_argument("--min-seg-kib", type=int, default=4,
-                    help="min-variable-segment-size (minLen = KiB*1024-1; 4 = the reference default)")
-    ap.add_argument("--mask-bits", type=int, default=12,
-                    help="boundary predicate (fp & (2^bits-1)) == 0 (12 = the default knob, SURVEY.md A.3)")
-    ap.add_argument("--at-4k", type=int, default=1, help="also time the 4 KiB-mean mix (minLen 2047, 11-bit)")
+    ap.add_argument("--threads", default="auto",
+                    help="getChunks caller-thread counts for the coalescing-queue sweep ('' = skip; auto = "
+                         "1,8,32,3 x the CPU quota (SDFS's default write-threads, Main.java:211-212),64,128,256)")
+    ap.add_argument("--threads-mode", default="fill", choices=["fill", "copy"],
+                    help="fill: the JNI glue's entry point (the byte[] copied once, into pinned staging)")
+    ap.add_argument("--min-seg-kib", type=int, default=2,
+                    help="min-variable-segment-size (minLen = KiB*1024-1; 2 = the metric's 4 KiB-mean mix, "
+                         "4 = the reference default)")
+    ap.add_argument("--mask-bits", type=int, default=11,
+                    help="boundary predicate (fp & (2^bits-1)) == 0 (11 = the 4 KiB-mean mix, 12 = the default "
+                         "knob, SURVEY.md A.3)")
+    ap.add_argument("--other-mix", type=int, default=1,
+                    help="also time the other mix (the reference default beside the 4 KiB mean, or vice versa)")
     ap.add_argument("--hash-type", default="VARIABLE_SHA256",
                     choices=["VARIABLE_SHA256", "VARIABLE_SHA256_160", "VARIABLE_MD5"])
     ap.add_argument("--ramp-secs", type=float, default=0.3, help="untimed clock ramp before the warmup steps")
@@ -217,7 +352,13 @@ def main():
                     help="direct: the engine writes records into the exchange slot; copy: snapshot copy")
     args = ap.parse_args()
 
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if launched and world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks (WORLD_SIZE); they must agree")
+        sys.exit(2)
+    if not launched and args.gpus > 1:
+        return main_device_set(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -330,10 +471,13 @@ def main():
         other = {"streams_in_flight": 1 if nsf >= 2 else 2, "value": round(nbytes * args.steps / el / 2**30, 3),
                  "ms_per_step": round(el / args.steps * 1e3, 4)}
 
-    # the metric's 4 KiB-mean mix: minLen 2047 (min-variable-segment-size=2) + 11-bit predicate
-    at4k = None
-    if world == 1 and args.at_4k:
-        cfg4 = SdfsConfig(chunk_length=buf_len, min_len=2047, pred_mask=0x7FF, hash_type=args.hash_type)
+    # the other chunk mix beside the headline: the reference default (minLen 4095, 12-bit) when
+    # the headline is the metric's 4 KiB-mean mix (minLen 2047, 11-bit), and vice versa
+    other_mix = None
+    main_is_4k = (cfg.min_len, cfg.pred_mask) == (2047, 0x7FF)
+    if world == 1 and args.other_mix:
+        om_min, om_mask = (4095, 0xFFF) if main_is_4k else (2047, 0x7FF)
+        cfg4 = SdfsConfig(chunk_length=buf_len, min_len=om_min, pred_mask=om_mask, hash_type=args.hash_type)
         e4 = HashFunctionPool(cfg4, device=local).getHashEngine()
         b4 = DeviceBatch(e4, nbuf=nbuf, buf_len=buf_len, device=device)
         b4.data = batch.data
@@ -348,10 +492,12 @@ def main():
         k4 = e4.kernel_times()
         e4.set_timing(0)
         tot4 = int(b4.total.item())
-        at4k = {"value": round(nbytes * args.steps / el / 2**30, 3), "ms_per_step": round(el / args.steps * 1e3, 4),
-                "params": "minLen=2047 (min-variable-segment-size=2) pred=(fp&0x7ff)==0 n>minLen",
-                "mean_chunk_bytes": round(nbytes / max(tot4, 1), 1), "chunks_per_gpu_step": tot4,
-                "kernels_ms": {k: round(v, 4) for k, v in k4.items() if v}, "records_identical": r4.identical()}
+        other_mix = {"value": round(nbytes * args.steps / el / 2**30, 3),
+                     "ms_per_step": round(el / args.steps * 1e3, 4),
+                     "params": f"minLen={om_min} pred=(fp&{om_mask:#x})==0 n>minLen"
+                               + (" (reference defaults)" if main_is_4k else " (min-variable-segment-size=2)"),
+                     "mean_chunk_bytes": round(nbytes / max(tot4, 1), 1), "chunks_per_gpu_step": tot4,
+                     "kernels_ms": {k: round(v, 4) for k, v in k4.items() if v}, "records_identical": r4.identical()}
         del r4, b4
         e4.destroy()
 
@@ -381,7 +527,15 @@ def main():
             e2e_pinned = nb * buf_len * reps / (time.perf_counter() - te) / 2**30
             del hp, hpn
         if args.threads:
-            sweep = threads_sweep(cfg, local, host, buf_len, [int(x) for x in args.threads.split(",") if x])
+            if args.threads == "auto":
+                # SDFS's default write-threads is 3 x availableProcessors (Main.java:211-212): on
+                # the GPU box a job's share is its cgroup quota
+                q = cpu_quota()
+                wt = 3 * int(q if q else min(16, len(os.sched_getaffinity(0))))
+                tl = sorted({1, 8, 32, wt, 64, 128, 256})
+            else:
+                tl = [int(x) for x in args.threads.split(",") if x]
+            sweep = threads_sweep(cfg, local, host, buf_len, tl, args.threads_mode)
 
     if rank != 0:
         if dist.is_initialized():
@@ -460,7 +614,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "one_stream" if nsf >= 2 else "two_streams": other,
-        "at_4k_mean": at4k,
+        ("at_ref_default" if main_is_4k else "at_4k_mean"): other_mix,
         "e2e_host_gibps": round(e2e, 3) if e2e else None,
         "e2e_pinned_host_gibps": round(e2e_pinned, 3) if e2e_pinned else None,
         "e2e_getchunks_threads": sweep,

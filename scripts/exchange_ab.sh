@@ -8,7 +8,7 @@ OUT=${1:-gpurun_out/exchange}
 REPS=${2:-2}
 mkdir -p "$OUT"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-X="--threads= --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --at-4k 0 --compare 0 --steps 30 --warmup 5"
+X="--threads= --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --other-mix 0 --compare 0 --steps 30 --warmup 5"
 P=29611
 for r in $(seq "$REPS"); do
   for mode in none copy direct; do

@@ -6,7 +6,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 1
 mkdir -p gpurun_out/final
 export TMPDIR=/tmp
-BENCH_ABS="python3 $R/bench.py --steps 20 --warmup 3 --e2e-mib 0 --threads= --at-4k 0 --cpu-secs 0 --cpu-1t-secs 0 --compare 0"
+BENCH_ABS="python3 $R/bench.py --steps 20 --warmup 3 --e2e-mib 0 --threads= --other-mix 0 --cpu-secs 0 --cpu-1t-secs 0 --compare 0"
 bash scripts/gpu_session.sh \
   "smoke:180:python3 -c 'import __graft_entry__ as g; g.smoke()'" \
   "prof:300:cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/final/prof -- $BENCH_ABS > $R/gpurun_out/final/bench_under_rocprof.log 2>&1" \

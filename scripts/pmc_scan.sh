@@ -7,7 +7,9 @@ set -o pipefail
 OUT=${1:-gpurun_out/pmc}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-B=${PMC_CMD:-"python3 bench.py --steps 6 --warmup 2 --threads= --at-4k 0 --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --compare 0 --streams-in-flight 1 --ramp-secs 0"}
+# MIX_ARGS picks the chunk mix (default: the bench's headline, the 4 KiB-mean mix; the reference
+# default is "--min-seg-kib 4 --mask-bits 12")
+B=${PMC_CMD:-"python3 bench.py --steps 6 --warmup 2 --threads= --other-mix 0 --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --compare 0 --streams-in-flight 1 --ramp-secs 0 ${MIX_ARGS:-}"}
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -- $B > "$OUT/$name.log" 2>&1

@@ -58,9 +58,7 @@ def main():
     a = ap.parse_args()
     fetch = read_counter(a.fetch_dir, "FETCH_SIZE")
     write = read_counter(a.write_dir, "WRITE_SIZE")
-    out = {"_note": "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024, mean over launches "
-                    "after warmup; FETCH_SIZE/WRITE_SIZE in KiB (rocprofv3, gfx950 x2 read correction)",
-           "params": a.params, "source": a.source, "commit": a.commit}
+    out = {"params": a.params, "source": a.source, "commit": a.commit}
     for stage in sorted(set(fetch) | set(write)):
         f = fetch.get(stage, [])[a.skip:] or fetch.get(stage, [])
         w = write.get(stage, [])[a.skip:] or write.get(stage, [])
@@ -72,8 +70,20 @@ def main():
             "write_size_kib": round(wk, 1),
             "hbm_bytes_per_launch": int((2 * fk + wk) * 1024),
         }
+    # one entry per measured chunk mix (the bench's params string), merged into the file
+    try:
+        doc = json.load(open(a.out))
+    except Exception:
+        doc = {}
+    by = doc.get("by_params", {})
+    if "params" in doc and doc["params"] not in by:  # the round-2 single-mix layout
+        by[doc["params"]] = {k: v for k, v in doc.items() if k not in ("_note", "by_params")}
+    by[a.params] = out
+    doc = {"_note": "per chunk mix (bench.py config.params): hbm_bytes_per_launch = (2*FETCH_SIZE + "
+                    "WRITE_SIZE) * 1024, mean over launches after warmup; FETCH_SIZE/WRITE_SIZE in KiB "
+                    "(rocprofv3, gfx950 x2 read correction)", "by_params": by}
     with open(a.out, "w") as fh:
-        json.dump(out, fh, indent=1)
+        json.dump(doc, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 

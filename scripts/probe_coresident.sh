@@ -5,7 +5,7 @@
 # workgroup (hash sweep variant 30).  Interleaved, twice.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export SDFS_CDC_LIB=$PWD/sdfs_amd/libsdfs_cdc_tuning.so
-Q="--threads= --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --at-4k 0 --compare 0"
+Q="--threads= --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --other-mix 0 --compare 0"
 bash scripts/gpu_session.sh \
   "base1:120:python bench.py $Q" \
   "both1:120:SDFS_SCAN_MAX_BLOCK=512 SDFS_HASH_VARIANT=30 python bench.py $Q" \

@@ -11,7 +11,7 @@ REPS=${2:-2}
 WIDTHS=${3:-"1024 512"}
 mkdir -p "$OUT"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-X="--threads= --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --at-4k 0 --steps 30 --warmup 5"
+X="--threads= --e2e-mib 0 --cpu-secs 0 --cpu-1t-secs 0 --other-mix 0 --steps 30 --warmup 5"
 for r in $(seq "$REPS"); do
   for spec in $WIDTHS; do
     IFS=: read -r w hv wpc <<< "$spec"

@@ -253,3 +253,65 @@ class ShardedDedupIndex:
         out_dup[order] = back_dup
         out_loc[order] = back_loc
         return out_dup, out_loc
+
+
+# ---- one process driving a device set (include/sdfs_cdc.h "Devices") ------------------------
+
+class DeviceSetExchange:
+    """The fingerprint-table exchange of ONE engine spanning several GPUs in one process: the
+    engine all-gathers its devices' record tables itself, over RCCL (xGMI), with one communicator
+    per device (``sdfs_cdc_allgather_records``) — the in-process counterpart of
+    :class:`RecordExchange` (one rank per GPU over torch.distributed).
+
+    Pipelined one step behind production: ``acquire(i, d, stream)`` hands device d the record slot
+    of step i (a ring of ``slots``) and orders ``stream`` after that slot's previous exchange;
+    ``produced(i, d, total, stream)`` marks step i's table on device d complete (an event on the
+    producer stream); ``exchange(i)`` — called after step i+1 has been launched, so the devices
+    stay busy — runs the exchange of step i on a side stream per device.  The call blocks only for
+    step i's counts.  Results: ``(counts, stride)`` per step; gathered tables in ``gathered[d][i %
+    2]`` (device j's rows at j * stride)."""
+
+    def __init__(self, engine, capacity: int, devices, slots: int = 3):
+        self.engine = engine
+        self.devices = [torch.device(d) for d in devices]
+        n = len(self.devices)
+        self.capacity = int(capacity)
+        self.nslots = slots
+        self.slots = [[torch.empty(self.capacity, RECORD_BYTES, dtype=torch.uint8, device=dv) for _ in range(slots)]
+                      for dv in self.devices]
+        self.gathered = [[torch.empty(n * self.capacity, RECORD_BYTES, dtype=torch.uint8, device=dv) for _ in range(2)]
+                         for dv in self.devices]
+        self.side = [torch.cuda.Stream(dv) for dv in self.devices]
+        self.free = [[None] * slots for _ in self.devices]      # side-stream event: slot's exchange done
+        self.prod = [[None] * slots for _ in self.devices]      # producer event: slot's table written
+        self.totals = [[None] * slots for _ in self.devices]    # the step's device count tensor
+        self.results = []
+
+    def acquire(self, i: int, d: int, stream) -> torch.Tensor:
+        k = i % self.nslots
+        if self.free[d][k] is not None:
+            stream.wait_event(self.free[d][k])
+            self.free[d][k] = None
+        return self.slots[d][k]
+
+    def produced(self, i: int, d: int, total: torch.Tensor, stream) -> None:
+        k = i % self.nslots
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self.prod[d][k] = ev
+        self.totals[d][k] = total
+
+    def exchange(self, i: int):
+        k = i % self.nslots
+        for d, s in enumerate(self.side):
+            s.wait_event(self.prod[d][k])
+        res = self.engine.allgather_records([self.slots[d][k] for d in range(len(self.devices))],
+                                            [self.totals[d][k] for d in range(len(self.devices))],
+                                            [self.gathered[d][i % 2] for d in range(len(self.devices))],
+                                            streams=[s.cuda_stream for s in self.side])
+        for d, s in enumerate(self.side):
+            ev = torch.cuda.Event()
+            ev.record(s)
+            self.free[d][k] = ev
+        self.results.append(res)
+        return res

@@ -48,10 +48,12 @@ def _check(res, data, nbuf, prm=None):
 
 
 def test_instances_share_one_engine_and_its_gpu_passes():
+    # (other tests of this process may hold instances of the same parameters: counts are relative)
     engines = [HipVariableSha256HashEngine() for _ in range(4)]
-    assert all(e.share_count() == 4 for e in engines)
-    other = HipVariableSha256HashEngine(config=SdfsConfig(min_len=2047, pred_mask=0x7FF))
-    assert other.share_count() == 1  # other parameters: an engine of its own
+    k = engines[0].share_count()
+    assert k >= 4 and all(e.share_count() == k for e in engines)
+    other = HipVariableSha256HashEngine(config=SdfsConfig(min_len=2047, pred_mask=0x7FF, max_len=32000))
+    assert other.share_count() == 1 and engines[0].share_count() == k  # other parameters: its own engine
     b0, r0 = engines[0].queue_stats()
     nbuf = 192
     data = _buffers(nbuf, 9100)
@@ -65,7 +67,7 @@ def test_instances_share_one_engine_and_its_gpu_passes():
     assert engines[3].queue_stats() == (b1, r1)
     for e in engines[:3]:
         e.destroy()
-    assert engines[3].share_count() == 1
+    assert engines[3].share_count() == k - 3
     st, ln, dg = engines[3].chunk_arrays(data[:L], fill=True)
     es, el, ed = O.chunk(data[:L])
     assert st.tolist() == es.tolist() and ln.tolist() == el.tolist() and (dg == ed).all()
@@ -78,6 +80,7 @@ def test_destroy_while_other_threads_are_in_calls():
     results, later calls on it fail with EINVAL, the other handle of the engine is unaffected."""
     a = HipVariableSha256HashEngine()
     b = HipVariableSha256HashEngine()
+    k = b.share_count()
     lib = _lib.load()
     ha = a._h
     bufs = [O.synth(O.SYNTH_SEED, 9300 + i, 0, L).tobytes() for i in range(8)]
@@ -120,7 +123,7 @@ def test_destroy_while_other_threads_are_in_calls():
         t.join()
     assert not errors, errors[:5]
     assert refused[0] > 0 and done[0] > 50
-    assert b.share_count() == 1
+    assert b.share_count() == k - 1
     b.destroy()
 
 

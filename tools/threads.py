@@ -54,6 +54,7 @@ def getchunks(engine, nthreads: int, data: np.ndarray, buf_len: int, total_calls
     getChunks entry point ("copy" sdfs_cdc_get_chunks, "fill" the JNI glue's
     sdfs_cdc_get_chunks_fill, "stream" sdfs_cdc_get_chunks_stream keyed by buffer // 16)."""
     lib = load()
+    engine = engine or engines[0]
     data = np.ascontiguousarray(data, np.uint8)
     nbuf = data.size // buf_len
     cap = engine.slot_cap(buf_len)
