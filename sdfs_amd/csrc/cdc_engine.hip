@@ -6,6 +6,7 @@
 // (VariableSha256HashEngine.java:41-121, VariableMD5HashEngine.java:37-108).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -1429,6 +1430,12 @@ std::string share_key(const sdfs_cdc_params* p, const std::vector<int>& ords) {
              (unsigned long long)p->max_batch_bytes);
     std::string k(buf);
     for (int o : ords) k += std::to_string(o) + ",";
+#ifdef SDFS_TUNING
+    // measurement build: engines created under different SDFS_* settings (A/B in one process,
+    // scripts/ab.py) must not share
+    for (char** ev = ::environ; ev && *ev; ev++)
+        if (strncmp(*ev, "SDFS_", 5) == 0) k += std::string("|") + *ev;
+#endif
     return k;
 }
 

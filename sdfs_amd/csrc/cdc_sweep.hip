@@ -119,6 +119,130 @@ hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant,
     }
 }
 
+// ---- two chunks per lane (variant 40/41): two independent SHA-256 chains interleaved round by
+// round in one lane, for twice the instruction-level parallelism per wave at ~1.5x the VGPRs.
+// Lane l of workgroup g takes tasks 2(256g+l) and 2(256g+l)+1: adjacent in the longest-first
+// list, so (binned by exact block count) their block counts are equal or differ by one.
+__device__ __forceinline__ void sha_round_pair(uint32_t (&x)[8], uint32_t (&y)[8], uint32_t k, uint32_t wx, uint32_t wy) {
+    {
+        const uint32_t S1 = xor3(rotr(x[4], 6), rotr(x[4], 11), rotr(x[4], 25));
+        const uint32_t ch = (x[4] & x[5]) | (~x[4] & x[6]);
+        const uint32_t t1 = x[7] + S1 + ch + k + wx;
+        const uint32_t S0 = xor3(rotr(x[0], 2), rotr(x[0], 13), rotr(x[0], 22));
+        const uint32_t mj = maj3(x[0], x[1], x[2]);
+        x[7] = x[6]; x[6] = x[5]; x[5] = x[4]; x[4] = x[3] + t1; x[3] = x[2]; x[2] = x[1]; x[1] = x[0]; x[0] = t1 + S0 + mj;
+    }
+    {
+        const uint32_t S1 = xor3(rotr(y[4], 6), rotr(y[4], 11), rotr(y[4], 25));
+        const uint32_t ch = (y[4] & y[5]) | (~y[4] & y[6]);
+        const uint32_t t1 = y[7] + S1 + ch + k + wy;
+        const uint32_t S0 = xor3(rotr(y[0], 2), rotr(y[0], 13), rotr(y[0], 22));
+        const uint32_t mj = maj3(y[0], y[1], y[2]);
+        y[7] = y[6]; y[6] = y[5]; y[5] = y[4]; y[4] = y[3] + t1; y[3] = y[2]; y[2] = y[1]; y[1] = y[0]; y[0] = t1 + S0 + mj;
+    }
+}
+
+__device__ __forceinline__ void sha_sched16(uint32_t (&w)[16]) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+        const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+        w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+    }
+}
+
+// One 64-byte block of one chunk as 16 big-endian words: data block, tail block(s), or zeros.
+__device__ __forceinline__ void pair_block_words(uint32_t (&w)[16], const uint4 (&v)[4], uint32_t blk, uint32_t nfull,
+                                                 uint32_t nblocks, const uint8_t* p, uint32_t len) {
+    if (blk < nfull) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            w[4 * q] = __builtin_bswap32(v[q].x);
+            w[4 * q + 1] = __builtin_bswap32(v[q].y);
+            w[4 * q + 2] = __builtin_bswap32(v[q].z);
+            w[4 * q + 3] = __builtin_bswap32(v[q].w);
+        }
+    } else {
+        if (blk == nfull) {
+            tail_words<true>(w, p + 64 * nfull, len & 63);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) w[j] = 0;
+        }
+        if (blk == nblocks - 1) {
+            const uint64_t bits = (uint64_t)len * 8;
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
+        }
+    }
+}
+
+template <bool PRIO, int WPE = 3>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void chunk_hash_pair_kernel(HashArgs a) {
+    const uint32_t total = *a.total;
+    const uint32_t i0 = 2 * (blockIdx.x * 256 + threadIdx.x);
+    if (i0 >= total) return;
+    const bool has1 = i0 + 1 < total;
+    uint32_t slot[2], b[2], k[2], cs[2], len[2], nfull[2], nblocks[2];
+    const uint8_t* p[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const uint32_t i = c == 0 || has1 ? i0 + c : i0;  // a missing second task repeats the first
+        slot[c] = a.tasks[i];
+        b[c] = slot[c] / a.cap;
+        k[c] = slot[c] - b[c] * a.cap;
+        const uint64_t boff = a.uniform_len ? (uint64_t)b[c] * a.uniform_len : a.offs[b[c]];
+        cs[c] = a.starts[slot[c]];
+        len[c] = a.clens[slot[c]];
+        p[c] = a.data + boff + cs[c];
+        nfull[c] = len[c] >> 6;
+        nblocks[c] = (len[c] + 8) / 64 + 1;
+    }
+    if constexpr (PRIO) {
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(nblocks[0]);
+        if (nb > 1024) __builtin_amdgcn_s_setprio(3);
+        else if (nb > 512) __builtin_amdgcn_s_setprio(2);
+        else if (nb > 256) __builtin_amdgcn_s_setprio(1);
+    }
+    uint32_t x[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint32_t y[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    const uint32_t nbmax = nblocks[0] > nblocks[1] ? nblocks[0] : nblocks[1];
+    for (uint32_t blk = 0; blk < nbmax; blk++) {
+        uint4 v0[4], v1[4];
+        load_block64(v0, blk < nfull[0] ? p[0] + 64 * blk : a.zero_page);
+        load_block64(v1, blk < nfull[1] ? p[1] + 64 * blk : a.zero_page);
+        uint32_t w0[16], w1[16];
+        pair_block_words(w0, v0, blk, nfull[0], nblocks[0], p[0], len[0]);
+        pair_block_words(w1, v1, blk, nfull[1], nblocks[1], p[1], len[1]);
+        uint32_t u[8], z[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) { u[j] = x[j]; z[j] = y[j]; }
+#pragma clang loop unroll(full)
+        for (int r = 0; r < 64; r++) {
+            if (r >= 16 && (r & 15) == 0) {
+                asm("" : "+v"(w0[0]), "+v"(w0[1]), "+v"(w0[2]), "+v"(w0[3]), "+v"(w0[4]), "+v"(w0[5]), "+v"(w0[6]),
+                    "+v"(w0[7]), "+v"(w0[8]), "+v"(w0[9]), "+v"(w0[10]), "+v"(w0[11]), "+v"(w0[12]), "+v"(w0[13]),
+                    "+v"(w0[14]), "+v"(w0[15]) : "v"(u[0]));
+                sha_sched16(w0);
+                asm("" : "+v"(w1[0]), "+v"(w1[1]), "+v"(w1[2]), "+v"(w1[3]), "+v"(w1[4]), "+v"(w1[5]), "+v"(w1[6]),
+                    "+v"(w1[7]), "+v"(w1[8]), "+v"(w1[9]), "+v"(w1[10]), "+v"(w1[11]), "+v"(w1[12]), "+v"(w1[13]),
+                    "+v"(w1[14]), "+v"(w1[15]) : "v"(z[0]));
+                sha_sched16(w1);
+            }
+            sha_round_pair(u, z, kSha256K[r], w0[r & 15], w1[r & 15]);
+        }
+        const bool live0 = blk < nblocks[0], live1 = blk < nblocks[1];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            x[j] = live0 ? x[j] + u[j] : x[j];
+            y[j] = live1 ? y[j] + z[j] : y[j];
+        }
+    }
+    store_digest<0>(a, slot[0], b[0], k[0], cs[0], len[0], x);
+    if (has1) store_digest<0>(a, slot[1], b[1], k[1], cs[1], len[1], y);
+}
+
 // fingerprint-kernel variants (SHA-256 only)
 hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t s) {
     const uint32_t blocks = (uint32_t)((max_tasks + 255) / 256);
@@ -162,6 +286,10 @@ hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant,
     case 22: hipLaunchKernelGGL((chunk_hash_kernel<0, 48, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
     case 23: hipLaunchKernelGGL((chunk_hash_kernel<0, 48, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
     case 24: hipLaunchKernelGGL((chunk_hash_kernel<0, 48, 256, true, true, 6>), dim3(blocks), dim3(256), 0, s, a); break;
+    // two chunks per lane (twice the ILP per wave), without / with the long-chunk issue priority
+    case 40: hipLaunchKernelGGL((chunk_hash_pair_kernel<false>), dim3((blocks + 1) / 2), dim3(256), 0, s, a); break;
+    case 41: hipLaunchKernelGGL((chunk_hash_pair_kernel<true>), dim3((blocks + 1) / 2), dim3(256), 0, s, a); break;
+    case 42: hipLaunchKernelGGL((chunk_hash_pair_kernel<true, 2>), dim3((blocks + 1) / 2), dim3(256), 0, s, a); break;
     // the prefetch before ABL bit 16 (its copy at the data/tail merge waited for the load)
     case 20: hipLaunchKernelGGL((chunk_hash_kernel<0, 0, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
     default: return hipErrorInvalidValue;
