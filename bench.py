@@ -348,6 +348,9 @@ def main():
     ap.add_argument("--compare", type=int, default=1, help="also time the other streams-in-flight mode (N = 1)")
     ap.add_argument("--exchange", type=int, default=-1,
                     help="record all-gather: -1 = when N > 1, 1 = also at N = 1 (exercises the path)")
+    ap.add_argument("--inproc", type=int, default=0,
+                    help="1: drive the GPUs from ONE process through a device-set engine even at N = 1 "
+                         "(the default for N > 1 without a launcher)")
     ap.add_argument("--exchange-mode", default="direct", choices=["direct", "copy"],
                     help="direct: the engine writes records into the exchange slot; copy: snapshot copy")
     args = ap.parse_args()
@@ -357,7 +360,7 @@ def main():
     if launched and world != args.gpus:
         log(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks (WORLD_SIZE); they must agree")
         sys.exit(2)
-    if not launched and args.gpus > 1:
+    if not launched and (args.gpus > 1 or args.inproc):
         return main_device_set(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

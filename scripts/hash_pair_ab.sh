@@ -8,4 +8,5 @@ bash scripts/gpu_session.sh \
  "b_base:120:python3 bench.py $Q" \
  "b_p41:120:SDFS_HASH_VARIANT=41 python3 bench.py $Q" \
  "b_base2:120:python3 bench.py $Q" \
- "b_p41b:120:SDFS_HASH_VARIANT=41 python3 bench.py $Q"
+ "b_p41b:120:SDFS_HASH_VARIANT=41 python3 bench.py $Q" \
+ "inproc:120:unset SDFS_CDC_LIB; python3 bench.py --inproc 1 --steps 20"
