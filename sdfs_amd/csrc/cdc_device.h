@@ -61,8 +61,8 @@ __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t d
         // (rev8(o) << 8) | c8; a byte already at bits 8..15 needs only the full-rate v_bitop3
         const uint32_t qa = Q == 2 ? bitop3_and_or(odw, 0xFF00u, c8)
                                    : __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + 3 - Q) << 8));
-        const uint2 pv = *reinterpret_cast<const uint2*>(tab + pa);
-        const uint2 qv = *reinterpret_cast<const uint2*>(tab + qa);
+        const uint2 pv = (ABL & 2) ? make_uint2(pa, pa >> 3) : *reinterpret_cast<const uint2*>(tab + pa);
+        const uint2 qv = (ABL & 1) ? make_uint2(qa, qa >> 3) : *reinterpret_cast<const uint2*>(tab + qa);
         const uint32_t nlo = __builtin_amdgcn_alignbit(hi, lo, 8);                      // R >> 8, low word
         const uint32_t nhi = __builtin_amdgcn_perm(hi, dw, 0x00070605u | ((3u - P) << 24));  // (hi >> 8) | rev8(b) << 24
         lo = xor3(nlo, pv.x, qv.x);
@@ -689,7 +689,8 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
                             cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
                         }
                     }
-                    block_words<W, PK, 0, BLK / 32, NCH, MB, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+                    block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 3) | MB, BLKW>(words, lo, hi, cur, prev, c8, push_base,
+                                                                                     tab, a);
                 }
             }
             if (!split_fast) {

@@ -41,6 +41,10 @@ using ScanV30 = ScanCfg<32, 1, false, 4, 16, 256, 2, kScanThreads, true>;
 using ScanV31 = ScanCfg<32, 1, false, 4, 16 | 128, 256, 2, kScanThreads, true>;
 // production with the candidate bits built from per-position SGPR masks (kAblSgprPred)
 using ScanV32 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred, 256, 2, kScanThreads, true>;
+// ablations of the production kernel (round 3): no pop read / no push read / neither
+using ScanV33 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | 1, 256, 2, kScanThreads, true>;
+using ScanV34 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | 2, 256, 2, kScanThreads, true>;
+using ScanV35 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | 3, 256, 2, kScanThreads, true>;
 using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;
 using ScanA2 = ScanCfg<32, 1, false, 4, 2, 128>;
 using ScanA3 = ScanCfg<32, 1, false, 4, 3, 128>;
@@ -86,6 +90,9 @@ ScanVariantInfo scan_variant_info_sweep(int v) {
     case 30: return sweep_info<ScanV30>();
     case 31: return sweep_info<ScanV31>();
     case 32: return sweep_info<ScanV32>();
+    case 33: return sweep_info<ScanV33>();
+    case 34: return sweep_info<ScanV34>();
+    case 35: return sweep_info<ScanV35>();
     default: return {0, 0, 0, 0, 0, 0, 0};
     }
 }
@@ -113,7 +120,8 @@ hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant,
     SWEEP_CASE(11, ScanA1) SWEEP_CASE(12, ScanA2) SWEEP_CASE(13, ScanA3) SWEEP_CASE(14, ScanA4)
     SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15) SWEEP_CASE(22, ScanV22) SWEEP_CASE(26, ScanV26)
     SWEEP_CASE(27, ScanV27) SWEEP_CASE(28, ScanV28) SWEEP_CASE(29, ScanV29) SWEEP_CASE(30, ScanV30)
-    SWEEP_CASE(31, ScanV31) SWEEP_CASE(32, ScanV32)
+    SWEEP_CASE(31, ScanV31) SWEEP_CASE(32, ScanV32) SWEEP_CASE(33, ScanV33) SWEEP_CASE(34, ScanV34)
+    SWEEP_CASE(35, ScanV35)
 #undef SWEEP_CASE
     default: return hipErrorInvalidValue;
     }
