@@ -52,6 +52,12 @@ constexpr int kAblMirror = 64;
 // the SGPR pair); a group without one is a single v_lshlrev.  1 -> ~0.25 VALU per byte for the
 // candidate bits at a 12-bit predicate.
 constexpr int kAblSgprPred = 256;
+// ABL bit kAblFullBlocks (scan kernel only): the batch is uniform and every segment is a whole
+// number of blocks (uniform_len % seg_len == 0, seg_len % BLK == 0), so the block loop has no
+// guarded path: its loads are unconditional and hipcc waits for them per 64 bytes scanned
+// instead of for the whole block at a control-flow merge.  Lanes past the batch's last segment
+// (nblk == 0) read the batch's first block and discard what they compute.
+constexpr int kAblFullBlocks = 512;
 
 template <int P, int Q, int ABL = 0>
 __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
@@ -564,7 +570,7 @@ struct ScanCfg {
 
 template <int W, int PK, class CFG>
 __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
-    static_assert(!CFG::kMirror || (CFG::kChains == 1 && !CFG::kPrefetch), "mirrored state: one chain, no prefetch");
+    static_assert(!CFG::kMirror || !CFG::kPrefetch, "mirrored state: no prefetch");
     static_assert(CFG::kMirror || PK != 2, "the one-compare predicate needs the mirrored state");
     constexpr int MB = (CFG::kMirror ? kAblMirror : 0) | (CFG::kAbl & kAblSgprPred);
     constexpr int NCH = CFG::kChains;
@@ -669,7 +675,20 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
             bool nxt_full[NCH];
             uint32_t words[NCH][BLK / 32];
             bool split_fast = false;
-            if constexpr (CFG::kAbl & 16) {
+            if constexpr ((CFG::kAbl & kAblFullBlocks) != 0) {
+#pragma unroll
+                for (int c = 0; c < NCH; c++) {
+                    const uint4* p = reinterpret_cast<const uint4*>(a.data + start[c] + (uint64_t)BLK * blk);
+#pragma unroll
+                    for (int i = 0; i < BLKW / 4; i++) {
+                        const uint4 v = p[i];
+                        cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
+                    }
+                }
+                block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 3) | MB, BLKW>(words, lo, hi, cur, prev, c8, push_base,
+                                                                                 tab, a);
+                split_fast = true;
+            } else if constexpr (CFG::kAbl & 16) {
                 // split body: when every lane's block is whole, a branch of its own loads and
                 // scans it, so no control-flow merge sits between the loads and their uses (hipcc
                 // waits for all 16 loads at such a merge; here it waits per 64 bytes scanned).

@@ -245,6 +245,12 @@ struct DevEngine {
     bool scan_prio = false;                  // pre-fingerprint stages on a high-priority stream (tuning: SDFS_SCAN_PRIO)
     hipStream_t s_scan = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // Front-end order across streams (SDFS_FRONT_SERIAL): a batch's scan waits for the previous
+    // batch's prefix/scatter (whatever stream it ran on), so those one-workgroup kernels never
+    // queue behind a full-chip scan of the other stream; the fingerprint kernels still overlap.
+    bool front_serial = false;
+    bool front_recorded = false;
+    hipEvent_t ev_front = nullptr;
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
@@ -425,6 +431,8 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     uint32_t* hist = w->small.p;
     uint32_t* cursor = w->small.p + kMaxBins;
     uint32_t* total = w->small.p + 2 * kMaxBins + 1;
+    const bool front = e->front_serial && e->ev_front && nbuf >= (uint32_t)e->num_cus * 4;
+    if (front && e->front_recorded) HIP_TRY(hipStreamWaitEvent(s, e->ev_front, 0));
     {
         const int t = t_begin(e, K_PREP, s);
         HIP_TRY(hipMemsetAsync(w->small.p, 0, (kSmall + 8) * sizeof(uint32_t), s));
@@ -552,6 +560,10 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
         const int t = t_begin(e, K_SCATTER, s);
         HIP_TRY(launch_scatter(ca, s));
         t_end(e, t, s);
+    }
+    if (front) {
+        HIP_TRY(hipEventRecord(e->ev_front, s));
+        e->front_recorded = true;
     }
     if (s != s_hash) {  // join: the fingerprint runs on the caller's stream
         HIP_TRY(hipEventRecord(e->ev_join, s));
@@ -1153,9 +1165,12 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
             hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
             return fail(SDFS_CDC_EHIP, "scan-priority stream creation failed");
     }
+    if (const char* v = getenv("SDFS_FRONT_SERIAL")) e->front_serial = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif
+    if (e->front_serial && hipEventCreateWithFlags(&e->ev_front, hipEventDisableTiming) != hipSuccess)
+        return fail(SDFS_CDC_EHIP, "event creation failed");
     e->scan_info = scan_variant_info(e->scan_variant);
     if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0)
         return fail(SDFS_CDC_EINVAL, "bad scan variant/segment length");
@@ -1212,7 +1227,7 @@ DevEngine::~DevEngine() {
             if (ev) (void)hipEventDestroy(ev);
     for (hipStream_t s : {e->stream, e->s_h2d, e->s_scan})
         if (s) (void)hipStreamDestroy(s);
-    for (hipEvent_t ev : {e->ev_fork, e->ev_join})
+    for (hipEvent_t ev : {e->ev_fork, e->ev_join, e->ev_front})
         if (ev) (void)hipEventDestroy(ev);
     for (hipStream_t s : e->qs)
         if (s) (void)hipStreamDestroy(s);

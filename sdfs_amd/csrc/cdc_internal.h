@@ -83,6 +83,11 @@ struct ScanArgs {
     uint32_t fuse_resolve;
     ResolveArgs res;
 };
+// Every segment of the batch is a whole number of `blk`-byte blocks (the scan kernel's
+// kAblFullBlocks form may run it).
+inline bool scan_full_blocks(const ScanArgs& a, uint32_t blk) {
+    return a.uniform_len != 0 && a.seg_len % blk == 0 && a.uniform_len % a.seg_len == 0;
+}
 
 
 struct PrefixArgs {

@@ -45,6 +45,12 @@ using ScanV32 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred, 256, 2, kScanThreads
 using ScanV33 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | 1, 256, 2, kScanThreads, true>;
 using ScanV34 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | 2, 256, 2, kScanThreads, true>;
 using ScanV35 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | 3, 256, 2, kScanThreads, true>;
+// production for batches of whole blocks only: no guarded load path in the block loop (kAblFullBlocks)
+using ScanV36 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | kAblFullBlocks, 256, 2, kScanThreads, true>;
+// two rolling chains per lane (more independent LDS round trips in flight per SIMD), 128-byte
+// blocks: 2 chains x 4 waves/SIMD (128 VGPRs) / 2 chains x 3 waves/SIMD (150 VGPRs)
+using ScanV37 = ScanCfg<32, 2, false, 4, 16 | kAblSgprPred | kAblFullBlocks, 128, 2, 1024, true>;
+using ScanV38 = ScanCfg<32, 2, false, 3, 16 | kAblSgprPred | kAblFullBlocks, 128, 2, 768, true>;
 using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;
 using ScanA2 = ScanCfg<32, 1, false, 4, 2, 128>;
 using ScanA3 = ScanCfg<32, 1, false, 4, 3, 128>;
@@ -93,12 +99,16 @@ ScanVariantInfo scan_variant_info_sweep(int v) {
     case 33: return sweep_info<ScanV33>();
     case 34: return sweep_info<ScanV34>();
     case 35: return sweep_info<ScanV35>();
+    case 36: return sweep_info<ScanV36>();
+    case 37: return sweep_info<ScanV37>();
+    case 38: return sweep_info<ScanV38>();
     default: return {0, 0, 0, 0, 0, 0, 0};
     }
 }
 
 template <class T>
 static hipError_t sweep_launch(const ScanArgs& a, int pk, int grid, int block, hipStream_t s) {
+    if ((T::kAbl & kAblFullBlocks) != 0 && !scan_full_blocks(a, T::kBlk)) return hipErrorInvalidValue;
     if (pk == 1)
         hipLaunchKernelGGL((cdc_scan_kernel<48, 1, T>), dim3(grid), dim3(block), 0, s, a);
     else if (pk == 2 && T::kMirror)
@@ -121,7 +131,8 @@ hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant,
     SWEEP_CASE(18, ScanA8) SWEEP_CASE(25, ScanA15) SWEEP_CASE(22, ScanV22) SWEEP_CASE(26, ScanV26)
     SWEEP_CASE(27, ScanV27) SWEEP_CASE(28, ScanV28) SWEEP_CASE(29, ScanV29) SWEEP_CASE(30, ScanV30)
     SWEEP_CASE(31, ScanV31) SWEEP_CASE(32, ScanV32) SWEEP_CASE(33, ScanV33) SWEEP_CASE(34, ScanV34)
-    SWEEP_CASE(35, ScanV35)
+    SWEEP_CASE(35, ScanV35) SWEEP_CASE(36, ScanV36) SWEEP_CASE(37, ScanV37)
+    SWEEP_CASE(38, ScanV38)
 #undef SWEEP_CASE
     default: return hipErrorInvalidValue;
     }
