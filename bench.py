@@ -536,9 +536,18 @@ def main():
                 q = cpu_quota()
                 wt = 3 * int(q if q else min(16, len(os.sched_getaffinity(0))))
                 tl = sorted({1, 8, 32, wt, 64, 128, 256})
+                tl_other = [1, wt]
             else:
                 tl = [int(x) for x in args.threads.split(",") if x]
+                tl_other = [1]
             sweep = threads_sweep(cfg, local, host, buf_len, tl, args.threads_mode)
+            if other_mix is not None:
+                # the other chunk mix's single-buffer latency at 1 thread and at SDFS's default
+                # write-threads (the engines of the two mixes differ only in minLen / predicate)
+                om_min, om_mask = (4095, 0xFFF) if main_is_4k else (2047, 0x7FF)
+                cfg_om = SdfsConfig(chunk_length=buf_len, min_len=om_min, pred_mask=om_mask, hash_type=args.hash_type)
+                other_mix["getchunks_threads"] = threads_sweep(cfg_om, local, host, buf_len,
+                                                               tl_other, args.threads_mode)
 
     if rank != 0:
         if dist.is_initialized():

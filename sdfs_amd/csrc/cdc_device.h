@@ -155,7 +155,9 @@ __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& 
     constexpr int OI = OLD >= 0 ? OLD : OLD + 64;
     const uint32_t odw = OLD >= 0 ? cur[OI >> 2] : prev[OI >> 2];
     roll_step<(O & 3), (OI & 3), ABL>(lo, hi, cur[O >> 2], odw, c8, push_base, a.jshift, tab);
-    if constexpr (ABL & 4) {
+    if constexpr ((ABL & 4) != 0 && (ABL & kAblSgprPred) != 0) {
+        asm volatile("" ::"v"(hi));  // round-3 form: the state stays live, no candidates at all
+    } else if constexpr (ABL & 4) {
         bits ^= lo;
     } else if constexpr ((ABL & kAblSgprPred) != 0 && (ABL & kAblMirror) != 0 && PK == 2) {
         asm("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(gm[O & 7]) : "s"(a.thr), "v"(hi));
@@ -685,7 +687,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
                         cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
                     }
                 }
-                block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 3) | MB, BLKW>(words, lo, hi, cur, prev, c8, push_base,
+                block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 7) | MB, BLKW>(words, lo, hi, cur, prev, c8, push_base,
                                                                                  tab, a);
                 split_fast = true;
             } else if constexpr (CFG::kAbl & 16) {

@@ -51,6 +51,13 @@ using ScanV36 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | kAblFullBlocks, 256
 // blocks: 2 chains x 4 waves/SIMD (128 VGPRs) / 2 chains x 3 waves/SIMD (150 VGPRs)
 using ScanV37 = ScanCfg<32, 2, false, 4, 16 | kAblSgprPred | kAblFullBlocks, 128, 2, 1024, true>;
 using ScanV38 = ScanCfg<32, 2, false, 3, 16 | kAblSgprPred | kAblFullBlocks, 128, 2, 768, true>;
+// more ablations of the production kernel (round 3): 4 = no candidate test (one v_xor per byte
+// instead of the SGPR-mask compare and its scalar OR / group branch), 8 = no global loads (block
+// words synthesized from registers; the guarded body), and their combinations with the LDS reads
+using ScanV39 = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | kAblFullBlocks | 4, 256, 2, kScanThreads, true>;
+using ScanV40 = ScanCfg<32, 1, false, 4, kAblSgprPred | 8, 256, 2, kScanThreads, true>;
+using ScanV41 = ScanCfg<32, 1, false, 4, kAblSgprPred | 4 | 8, 256, 2, kScanThreads, true>;
+using ScanV42 = ScanCfg<32, 1, false, 4, kAblSgprPred | 3 | 4 | 8, 256, 2, kScanThreads, true>;
 using ScanA1 = ScanCfg<32, 1, false, 4, 1, 128>;
 using ScanA2 = ScanCfg<32, 1, false, 4, 2, 128>;
 using ScanA3 = ScanCfg<32, 1, false, 4, 3, 128>;
@@ -102,6 +109,10 @@ ScanVariantInfo scan_variant_info_sweep(int v) {
     case 36: return sweep_info<ScanV36>();
     case 37: return sweep_info<ScanV37>();
     case 38: return sweep_info<ScanV38>();
+    case 39: return sweep_info<ScanV39>();
+    case 40: return sweep_info<ScanV40>();
+    case 41: return sweep_info<ScanV41>();
+    case 42: return sweep_info<ScanV42>();
     default: return {0, 0, 0, 0, 0, 0, 0};
     }
 }
@@ -132,7 +143,8 @@ hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant,
     SWEEP_CASE(27, ScanV27) SWEEP_CASE(28, ScanV28) SWEEP_CASE(29, ScanV29) SWEEP_CASE(30, ScanV30)
     SWEEP_CASE(31, ScanV31) SWEEP_CASE(32, ScanV32) SWEEP_CASE(33, ScanV33) SWEEP_CASE(34, ScanV34)
     SWEEP_CASE(35, ScanV35) SWEEP_CASE(36, ScanV36) SWEEP_CASE(37, ScanV37)
-    SWEEP_CASE(38, ScanV38)
+    SWEEP_CASE(38, ScanV38) SWEEP_CASE(39, ScanV39) SWEEP_CASE(40, ScanV40) SWEEP_CASE(41, ScanV41)
+    SWEEP_CASE(42, ScanV42)
 #undef SWEEP_CASE
     default: return hipErrorInvalidValue;
     }
