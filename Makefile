@@ -11,7 +11,7 @@ LIB := sdfs_amd/libsdfs_cdc.so
 TUNING_LIB := sdfs_amd/libsdfs_cdc_tuning.so
 SRCS := cdc_kernels cdc_engine dedup_index lz4_kernels map_emit aes_kernels
 OBJS := $(SRCS:%=build/%.o)
-TUNING_OBJS := $(SRCS:%=build/tuning/%.o) build/tuning/cdc_sweep.o
+TUNING_OBJS := $(SRCS:%=build/tuning/%.o) build/tuning/cdc_sweep.o build/tuning/cdc_sweep_r3.o
 HDRS := $(CSRC)/cdc_internal.h $(CSRC)/cdc_device.h $(CSRC)/host_queue.h $(CSRC)/engine_share.h $(CSRC)/stream_order.h $(wildcard include/*.h)
 
 all: $(LIB) tuning tools oracle

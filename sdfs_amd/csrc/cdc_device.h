@@ -59,20 +59,71 @@ constexpr int kAblSgprPred = 256;
 // (nblk == 0) read the batch's first block and discard what they compute.
 constexpr int kAblFullBlocks = 512;
 
+// ABL bit kAblSdwa (mirrored state): the push address is ONE v_lshrrev_b32_sdwa writing
+// (lo >> jshift) & 0xFF into byte 1 of a register that keeps push_base in its other bytes
+// (dst_unused:UNUSED_PRESERVE), instead of v_lshrrev + v_bitop3: one VALU less per byte, and one
+// dependent instruction less in the per-byte chain (index -> LDS read -> xor3 -> index).
+// kAblSdwaPop: the pop address the same way (v_mov_b32_sdwa of the outgoing byte into byte 1 of a
+// register holding c8) instead of v_perm / v_bitop3.
+constexpr int kAblSdwa = 1024;
+constexpr int kAblSdwaPop = 2048;
+// kAblMinGroup (mirrored state, low-k zero predicate; sweep only): candidate bits per group of 4
+// positions (kAblMinGroup8: 8) from the group's minimum predicate word, VALU only — no per-position
+// SGPR mask and no scalar OR chain (see byte_step).
+constexpr int kAblMinGroup = 4096;
+constexpr int kAblMinGroup8 = 8192;
+// kAblPopSwap (mirrored state): the pop-table entries are stored high word first, so the low-word
+// xor3 takes its pop operand from the ODD register of the ds_read_b64 destination pair.  VGPR
+// tuples are even-aligned on gfx950 and hipcc keeps handing both lookups' pairs and the shifted
+// low word registers of one bank (v54, v58, v62): a v_bitop3 whose three sources share a bank
+// issues in ~3.5 instead of ~2.2 cycles (scripts/vgpr_bank_microbench.hip).
+constexpr int kAblPopSwap = 16384;
+
+template <int B>
+__device__ __forceinline__ void sdwa_byte_to_b1(uint32_t& d, uint32_t src) {
+    static_assert(B >= 0 && B < 4, "byte select");
+    if constexpr (B == 0)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(d) : "v"(src));
+    else if constexpr (B == 1)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(d) : "v"(src));
+    else if constexpr (B == 2)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(d) : "v"(src));
+    else
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(d) : "v"(src));
+}
+
 template <int P, int Q, int ABL = 0>
-__device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t c8,
-                                          uint32_t push_base, uint32_t jshift, const uint8_t* tab) {
+__device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t dw, uint32_t odw, uint32_t& c8,
+                                          uint32_t& push_base, uint32_t jshift, const uint8_t* tab) {
     if constexpr ((ABL & kAblMirror) != 0) {
-        const uint32_t pa = bitop3_and_or(lo >> (jshift - 8), 0xFF00u, push_base);
-        // (rev8(o) << 8) | c8; a byte already at bits 8..15 needs only the full-rate v_bitop3
-        const uint32_t qa = Q == 2 ? bitop3_and_or(odw, 0xFF00u, c8)
-                                   : __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + 3 - Q) << 8));
+        uint32_t pa, qa;
+        if constexpr ((ABL & kAblSdwa) != 0) {
+            asm("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(push_base)
+                : "v"(lo), "s"(jshift));
+            pa = push_base;
+        } else {
+            pa = bitop3_and_or(lo >> (jshift - 8), 0xFF00u, push_base);
+        }
+        if constexpr ((ABL & kAblSdwaPop) != 0) {
+            sdwa_byte_to_b1<3 - Q>(c8, odw);
+            qa = c8;
+        } else {
+            // (rev8(o) << 8) | c8; a byte already at bits 8..15 needs only the full-rate v_bitop3
+            qa = Q == 2 ? bitop3_and_or(odw, 0xFF00u, c8)
+                        : __builtin_amdgcn_perm(odw, c8, 0x0C0C0000u | ((4u + 3 - Q) << 8));
+        }
         const uint2 pv = (ABL & 2) ? make_uint2(pa, pa >> 3) : *reinterpret_cast<const uint2*>(tab + pa);
         const uint2 qv = (ABL & 1) ? make_uint2(qa, qa >> 3) : *reinterpret_cast<const uint2*>(tab + qa);
         const uint32_t nlo = __builtin_amdgcn_alignbit(hi, lo, 8);                      // R >> 8, low word
         const uint32_t nhi = __builtin_amdgcn_perm(hi, dw, 0x00070605u | ((3u - P) << 24));  // (hi >> 8) | rev8(b) << 24
-        lo = xor3(nlo, pv.x, qv.x);
-        hi = xor3(nhi, pv.y, qv.y);
+        if constexpr ((ABL & kAblPopSwap) != 0) {
+            lo = xor3(nlo, pv.x, qv.y);
+            hi = xor3(nhi, pv.y, qv.x);
+        } else {
+            lo = xor3(nlo, pv.x, qv.x);
+            hi = xor3(nhi, pv.y, qv.y);
+        }
         return;
     }
     // push[j] address (j << 8) | push_base with j = (fp >> (d-8)) & 0xFF = hi bits [jshift, jshift+8):
@@ -149,8 +200,8 @@ __device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t
 // this block when O >= W, otherwise in `prev` (the previous block's last 64 bytes).
 template <int W, int PK, int O, int ABL, int BLKW>
 __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& bits, const uint32_t (&cur)[BLKW],
-                                          const uint32_t (&prev)[16], uint32_t c8, uint32_t push_base,
-                                          const uint8_t* tab, const ScanArgs& a, uint64_t (&gm)[8]) {
+                                          const uint32_t (&prev)[16], uint32_t& c8, uint32_t& push_base,
+                                          const uint8_t* tab, const ScanArgs& a, uint64_t (&gm)[8], uint32_t (&hv)[8]) {
     constexpr int OLD = O - W;  // may be negative -> previous block
     constexpr int OI = OLD >= 0 ? OLD : OLD + 64;
     const uint32_t odw = OLD >= 0 ? cur[OI >> 2] : prev[OI >> 2];
@@ -159,6 +210,26 @@ __device__ __forceinline__ void byte_step(uint32_t& lo, uint32_t& hi, uint32_t& 
         asm volatile("" ::"v"(hi));  // round-3 form: the state stays live, no candidates at all
     } else if constexpr (ABL & 4) {
         bits ^= lo;
+    } else if constexpr ((ABL & kAblMinGroup) != 0 && (ABL & kAblMirror) != 0 && PK == 2) {
+        // groups of G positions: the group's minimum predicate word decides (one v_min3 per two
+        // positions, one compare per group); only a group in which some lane has a candidate
+        // shifts its G exact bits in (v_cmp/v_addc), every other group is one shift by G
+        constexpr int G = (ABL & kAblMinGroup8) != 0 ? 8 : 4;
+        hv[O & (G - 1)] = hi;
+        if constexpr ((O & (G - 1)) == G - 1) {
+            uint32_t m = min(min(hv[0], hv[1]), hv[2]);
+            m = min(m, hv[3]);
+            if constexpr (G == 8) {
+                m = min(min(m, hv[4]), hv[5]);
+                m = min(min(m, hv[6]), hv[7]);
+            }
+            if (__builtin_expect(__any(m < a.thr), 0)) {
+#pragma unroll
+                for (int p = 0; p < G; p++) cand_shift<2>(bits, hv[p], 0u, a);
+            } else {
+                bits <<= G;
+            }
+        }
     } else if constexpr ((ABL & kAblSgprPred) != 0 && (ABL & kAblMirror) != 0 && PK == 2) {
         asm("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(gm[O & 7]) : "s"(a.thr), "v"(hi));
         if constexpr ((O & 7) == 7) {
@@ -224,22 +295,22 @@ constexpr int kSchedGroup = SDFS_SCAN_SCHED_GROUP;  // bytes per scheduling regi
 template <int W, int PK, int O0, int O, int NCH, int ABL, int BLKW>
 __device__ __forceinline__ void word_steps(uint32_t (&lo)[NCH], uint32_t (&hi)[NCH], uint32_t (&bits)[NCH],
                                            const uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
-                                           uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a,
-                                           uint64_t (&gm)[NCH][8]) {
+                                           uint32_t& c8, uint32_t& push_base, const uint8_t* tab, const ScanArgs& a,
+                                           uint64_t (&gm)[NCH][8], uint32_t (&hv)[NCH][8]) {
     if constexpr (O < O0 + 32) {
         if constexpr (NCH > 1 && ABL == 0) {
             bytes_multi<W, PK, O, NCH, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a);
         } else {
 #pragma unroll
             for (int c = 0; c < NCH; c++)
-                byte_step<W, PK, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a, gm[c]);
+                byte_step<W, PK, O, ABL, BLKW>(lo[c], hi[c], bits[c], cur[c], prev[c], c8, push_base, tab, a, gm[c], hv[c]);
         }
         if constexpr ((O & (kSchedGroup - 1)) == kSchedGroup - 1) {
             // keep the scheduler from hoisting every (chain-independent) pop read of the block
             // ahead of the rolling chain: that costs ~2 VGPRs per byte and spills.
             __builtin_amdgcn_sched_barrier(0);
         }
-        word_steps<W, PK, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a, gm);
+        word_steps<W, PK, O0, O + 1, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a, gm, hv);
     }
 }
 
@@ -278,7 +349,7 @@ __device__ __forceinline__ void load_block(uint32_t (&d)[N], const uint8_t* data
 template <int W, int PK, int WI, int NW, int NCH, int ABL, int BLKW>
 __device__ __forceinline__ void block_words(uint32_t (&words)[NCH][NW], uint32_t (&lo)[NCH], uint32_t (&hi)[NCH],
                                             uint32_t (&cur)[NCH][BLKW], const uint32_t (&prev)[NCH][16],
-                                            uint32_t c8, uint32_t push_base, const uint8_t* tab, const ScanArgs& a) {
+                                            uint32_t& c8, uint32_t& push_base, const uint8_t* tab, const ScanArgs& a) {
     if constexpr (WI < NW) {
         if constexpr ((ABL & kAblMirror) != 0) {
 #pragma unroll
@@ -288,9 +359,10 @@ __device__ __forceinline__ void block_words(uint32_t (&words)[NCH][NW], uint32_t
         }
         uint32_t bits[NCH];
         uint64_t gm[NCH][8];  // kAblSgprPred: the group's per-position compare masks (SGPR pairs)
+        uint32_t hv[NCH][8];  // kAblMinGroup: the group's predicate words (mirrored hi)
 #pragma unroll
         for (int c = 0; c < NCH; c++) bits[c] = 0;
-        word_steps<W, PK, 32 * WI, 32 * WI, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a, gm);
+        word_steps<W, PK, 32 * WI, 32 * WI, NCH, ABL, BLKW>(lo, hi, bits, cur, prev, c8, push_base, tab, a, gm, hv);
 #pragma unroll
         for (int c = 0; c < NCH; c++) words[c][WI] = __builtin_bitreverse32(bits[c]);
         block_words<W, PK, WI + 1, NW, NCH, ABL, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
@@ -558,6 +630,7 @@ template <int C, int NCH, bool PF, int WPS, int ABL = 0, int BLK = 64, int FUSE 
           bool MIRROR = false>
 struct ScanCfg {
     static constexpr bool kMirror = MIRROR;  // bit-reversed rolling state (roll_step, kAblMirror)
+    static constexpr bool kPopSwap = MIRROR && (ABL & kAblPopSwap) != 0;  // pop entries high word first
     static constexpr int kFuse = NCH == 1 ? FUSE : (FUSE == 2 ? 2 : 0);  // resolve each wave's buffer(s) in the epilogue
     static constexpr int kThreads = THREADS;
     static constexpr int kAbl = ABL;
@@ -574,7 +647,8 @@ template <int W, int PK, class CFG>
 __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
     static_assert(!CFG::kMirror || !CFG::kPrefetch, "mirrored state: no prefetch");
     static_assert(CFG::kMirror || PK != 2, "the one-compare predicate needs the mirrored state");
-    constexpr int MB = (CFG::kMirror ? kAblMirror : 0) | (CFG::kAbl & kAblSgprPred);
+    constexpr int MB =
+        (CFG::kMirror ? kAblMirror : 0) | (CFG::kAbl & (kAblSgprPred | kAblSdwa | kAblSdwaPop | kAblMinGroup | kAblMinGroup8 | kAblPopSwap));
     constexpr int NCH = CFG::kChains;
     constexpr int C = CFG::kCopies;
     constexpr int BLK = CFG::kBlk;
@@ -593,6 +667,9 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c8 = (lane & (C - 1)) << 3;
     const uint32_t push_base = CFG::kPushOff | c8;
+    // the block loop's address registers: the SDWA forms (kAblSdwa, kAblSdwaPop) rewrite byte 1
+    // of these in place, every other form only reads them
+    uint32_t pa_reg = push_base, qa_reg = c8;
     const uint64_t total = a.uniform_len ? a.total_segs : a.seg_prefix[a.nbuf];
     // workgroups of 64..1024 threads (a multiple of 64: a wave never straddles two buffers of the
     // fused walk); small batches launch narrow workgroups so their waves do not share SIMDs
@@ -687,7 +764,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
                         cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
                     }
                 }
-                block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 7) | MB, BLKW>(words, lo, hi, cur, prev, c8, push_base,
+                block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 7) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg,
                                                                                  tab, a);
                 split_fast = true;
             } else if constexpr (CFG::kAbl & 16) {
@@ -710,7 +787,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
                             cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
                         }
                     }
-                    block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 3) | MB, BLKW>(words, lo, hi, cur, prev, c8, push_base,
+                    block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 3) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg,
                                                                                      tab, a);
                 }
             }
@@ -730,7 +807,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
                     load_block<BLKW>(cur[c], a.data, act ? start[c] + (uint64_t)BLK * blk : 0, act ? end[c] : 0);
                 }
             }
-            block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 15) | MB, BLKW>(words, lo, hi, cur, prev, c8, push_base, tab, a);
+            block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 15) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg, tab, a);
             }
             if constexpr (CFG::kFuse == 2) {
                 // candidates are rare (~1 per 4 KiB): a divergent, seldom-taken append

@@ -82,7 +82,7 @@ uint32_t rev8_host(uint32_t v) { return (uint32_t)(bitrev64_host(v) >> 56); }
 // Rolling-hash tables (same definition as the jar's precompute), laid out as the
 // scan kernel's LDS image with `copies` lane-private copies (cdc_internal.h).  `mirror`: the
 // tables of the bit-reversed state (cdc_device.h roll_step): entry x = bitrev64(table[rev8(x)]).
-std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window, int copies, bool mirror) {
+std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window, int copies, bool mirror, bool pop_swap) {
     const int d = poly_degree(poly);
     std::vector<uint64_t> push(256), pop(256);
     for (uint64_t i = 0; i < 256; i++) {
@@ -101,6 +101,8 @@ std::vector<uint8_t> build_table_image(uint64_t poly, uint32_t window, int copie
         }
         push.swap(mpush);
         pop.swap(mpop);
+        if (pop_swap)  // high word first (the scan's kAblPopSwap forms)
+            for (uint64_t& v : pop) v = (v << 32) | (v >> 32);
     }
     std::vector<uint8_t> img(scan_lds_bytes(copies));
     const uint32_t push_off = copies == 32 ? 0x10000u : 0x80u;
@@ -1174,7 +1176,8 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     e->scan_info = scan_variant_info(e->scan_variant);
     if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0)
         return fail(SDFS_CDC_EINVAL, "bad scan variant/segment length");
-    std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies, e->scan_info.mirror != 0);
+    std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies, e->scan_info.mirror != 0,
+                                                 e->scan_info.pop_swap != 0);
     if (e->zero_page.ensure(256) != hipSuccess || hipMemset(e->zero_page.p, 0, 256) != hipSuccess ||
         e->tab_image.ensure(img.size()) != hipSuccess ||
         hipMemcpy(e->tab_image.p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess)

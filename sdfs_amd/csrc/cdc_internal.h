@@ -27,6 +27,7 @@ struct ScanVariantInfo {
                      // (sweep only), 2 = from register candidate summaries (production)
     int threads;     // widest workgroup the variant is compiled for
     int mirror;      // bit-reversed rolling state (mirrored LDS tables, one-compare predicate)
+    int pop_swap;    // pop-table entries stored high word first (kAblPopSwap: register banks)
 };
 ScanVariantInfo scan_variant_info(int variant);
 
@@ -179,6 +180,11 @@ bool scan_window_supported(int window);
 #ifdef SDFS_TUNING
 // measurement-only variants (cdc_sweep.hip; tuning library only)
 ScanVariantInfo scan_variant_info_sweep(int variant);
+// round-3 variants (cdc_sweep_r3.hip: a translation unit of its own, so that a new variant
+// compiles in a minute instead of rebuilding every earlier one)
+ScanVariantInfo scan_variant_info_sweep_r3(int variant);
+hipError_t launch_scan_sweep_r3(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
+                                hipStream_t s);
 hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
                              hipStream_t stream);
 hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);

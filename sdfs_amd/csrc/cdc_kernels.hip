@@ -29,12 +29,18 @@ namespace sdfs {
 // 8-position groups with a candidate pay for shifting their bits in (kAblSgprPred): ~8.6 instead
 // of 10.1 VALU per byte.  Interleaved A/B on MI355X against the alternatives is in DESIGN.md
 // §7-8 (sweep variants 29 = plain state, 30 = mirrored without the SGPR masks).
-using ScanProd = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred, 256, 2, kScanThreads, true>;
+// Since round 3 both LDS addresses are single SDWA instructions writing byte 1 of a register that
+// keeps the table base and lane offset in its other bytes (kAblSdwa, kAblSdwaPop): the push
+// address one v_lshrrev_b32_sdwa instead of v_lshrrev + v_bitop3 (one VALU less per byte and
+// one dependent instruction less in the rolling chain), the pop address one v_mov_b32_sdwa
+// instead of v_perm.  Interleaved A/B, identical records: 1.368 -> 1.245 ms per 4 GiB at the
+// 4 KiB-mean mix, 1.282 -> 1.162 at the reference default (sweep variant 32 = the form before).
+using ScanProd = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | kAblSdwa | kAblSdwaPop, 256, 2, kScanThreads, true>;
 
 template <class CFG>
 constexpr ScanVariantInfo info_of() {
     return {CFG::kCopies, CFG::kChains, CFG::kLds, std::max(1, CFG::kWavesPerSimd * 256 / CFG::kThreads), CFG::kBlk,
-            CFG::kFuse, CFG::kThreads, CFG::kMirror};
+            CFG::kFuse, CFG::kThreads, CFG::kMirror, CFG::kPopSwap};
 }
 
 ScanVariantInfo scan_variant_info(int v) {

@@ -113,7 +113,7 @@ ScanVariantInfo scan_variant_info_sweep(int v) {
     case 40: return sweep_info<ScanV40>();
     case 41: return sweep_info<ScanV41>();
     case 42: return sweep_info<ScanV42>();
-    default: return {0, 0, 0, 0, 0, 0, 0};
+    default: return scan_variant_info_sweep_r3(v);
     }
 }
 
@@ -146,7 +146,7 @@ hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant,
     SWEEP_CASE(38, ScanV38) SWEEP_CASE(39, ScanV39) SWEEP_CASE(40, ScanV40) SWEEP_CASE(41, ScanV41)
     SWEEP_CASE(42, ScanV42)
 #undef SWEEP_CASE
-    default: return hipErrorInvalidValue;
+    default: return launch_scan_sweep_r3(a, window, pk, variant, grid, block, s);
     }
 }
 
