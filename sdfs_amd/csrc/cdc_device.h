@@ -78,6 +78,9 @@ constexpr int kAblMinGroup8 = 8192;
 // low word registers of one bank (v54, v58, v62): a v_bitop3 whose three sources share a bank
 // issues in ~3.5 instead of ~2.2 cycles (scripts/vgpr_bank_microbench.hip).
 constexpr int kAblPopSwap = 16384;
+// kAblPopMux (with kAblSdwaPop): for the one byte in four whose bit-reversed copy already sits in
+// byte 1 of its dword, the pop address is a full-rate v_bitop3 bit-select instead of the SDWA move.
+constexpr int kAblPopMux = 32768;
 
 template <int B>
 __device__ __forceinline__ void sdwa_byte_to_b1(uint32_t& d, uint32_t src) {
@@ -105,7 +108,11 @@ __device__ __forceinline__ void roll_step(uint32_t& lo, uint32_t& hi, uint32_t d
         } else {
             pa = bitop3_and_or(lo >> (jshift - 8), 0xFF00u, push_base);
         }
-        if constexpr ((ABL & kAblSdwaPop) != 0) {
+        if constexpr ((ABL & kAblSdwaPop) != 0 && (ABL & kAblPopMux) != 0 && Q == 2) {
+            // the outgoing byte already sits in byte 1: one full-rate bit-select (B ? A : C)
+            // takes byte 1 from it and the rest (base, lane offset) from the address register
+            qa = __builtin_amdgcn_bitop3_b32(odw, 0xFF00u, c8, 0xE2);
+        } else if constexpr ((ABL & kAblSdwaPop) != 0) {
             sdwa_byte_to_b1<3 - Q>(c8, odw);
             qa = c8;
         } else {
@@ -643,16 +650,226 @@ struct ScanCfg {
     static constexpr int kBlk = BLK;
 };
 
+// One pass of the scan over the segments base + c * bdim + tid (c < chains) — one lane's share of
+// one iteration of the persistent scan kernel below; the fused scan + fingerprint kernel calls it
+// per wave with (buffer * 64, lane, 64).  With the fused cut walk, the wave's 64 segments are
+// buffer (base + (tid & ~63)) / 64.
+template <int W, int PK, class CFG>
+__device__ __forceinline__ void scan_iter(const ScanArgs& a, const uint8_t* tab, uint32_t* lhist, uint64_t base,
+                                          uint32_t tid, uint32_t bdim, uint64_t total, uint32_t lane, uint32_t c8,
+                                          uint32_t push_base, uint32_t& pa_reg, uint32_t& qa_reg) {
+    constexpr int MB =
+        (CFG::kMirror ? kAblMirror : 0) | (CFG::kAbl & (kAblSgprPred | kAblSdwa | kAblSdwaPop | kAblMinGroup | kAblMinGroup8 | kAblPopSwap | kAblPopMux));
+    constexpr int NCH = CFG::kChains;
+    constexpr int BLK = CFG::kBlk;
+    constexpr int BLKW = BLK / 4;
+    uint64_t start[NCH], end[NCH];
+    uint32_t nblk[NCH];
+    bool first[NCH];
+    uint32_t maxblk = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const uint64_t seg = base + (uint64_t)c * bdim + tid;
+        start[c] = end[c] = 0;
+        nblk[c] = 0;
+        first[c] = true;
+        if (seg < total) {
+            uint64_t bstart, blen, sidx;
+            if (a.uniform_len) {
+                const uint64_t spb = (a.uniform_len + a.seg_len - 1) / a.seg_len;
+                const uint64_t b = seg / spb;
+                sidx = seg - b * spb;
+                bstart = b * a.uniform_len;
+                blen = a.uniform_len;
+            } else {
+                uint32_t lo_b = 0, hi_b = a.nbuf;  // last b with seg_prefix[b] <= seg
+                while (hi_b - lo_b > 1) {
+                    const uint32_t mid = (lo_b + hi_b) >> 1;
+                    if (a.seg_prefix[mid] <= seg) lo_b = mid; else hi_b = mid;
+                }
+                sidx = seg - a.seg_prefix[lo_b];
+                bstart = a.offs[lo_b];
+                blen = a.lens[lo_b];
+            }
+            start[c] = bstart + sidx * a.seg_len;
+            const uint64_t bend = bstart + blen;
+            end[c] = start[c] + a.seg_len < bend ? start[c] + a.seg_len : bend;
+            nblk[c] = (uint32_t)((end[c] - start[c] + BLK - 1) / BLK);
+            // window warm-up reads the previous 64 bytes unless this is the buffer's first segment
+            first[c] = start[c] == bstart;
+        }
+        maxblk = nblk[c] > maxblk ? nblk[c] : maxblk;
+    }
+
+    uint32_t lo[NCH], hi[NCH];
+    uint32_t prev[NCH][16], cur[NCH][BLKW];
+    bool cur_full[NCH];
+    uint32_t sm[NCH][4];  // FUSE == 2: candidate summary per chain
+    uint32_t ncand[NCH];
+    uint32_t ovf_off[NCH];  // FUSE == 2: segment offset of the first stored bitmap block
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        sm[c][0] = sm[c][1] = sm[c][2] = sm[c][3] = 0xFFFFFFFFu;
+        ncand[c] = 0;
+        ovf_off[c] = 0xFFFFFFFFu;
+    }
+    // FUSE == 2 with the fused resolve: bitmap words are stored only once a lane's summary has
+    // overflowed (> kSumCands candidates), from that block on; resolve_from_summary reads them
+    // only there.  Saves the 0.5 GB of bitmap writes per 4 GiB.
+    const bool sparse_bm = CFG::kFuse == 2 && a.fuse_resolve;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        if (nblk[c] != 0 && !first[c]) {
+            load_block<16>(prev[c], a.data, start[c] - 64, start[c]);
+            if constexpr (CFG::kMirror)
+#pragma unroll
+                for (int i = 0; i < 16; i++) prev[c][i] = __builtin_bitreverse32(prev[c][i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) prev[c][i] = 0;  // bytes before the buffer are empty
+        }
+        lo[c] = hi[c] = 0;
+        warm_from<W, 64 - W, CFG::kMirror>(lo[c], hi[c], prev[c], push_base, a.jshift, tab);
+        if constexpr (CFG::kPrefetch) {
+            const bool act = nblk[c] != 0;
+            cur_full[c] = load_block_nb<BLKW>(cur[c], a.data, a.zero_page, act ? start[c] : 0, act ? end[c] : 0);
+        }
+    }
+
+    for (uint32_t blk = 0; blk < maxblk; blk++) {
+        uint32_t nxt[NCH][CFG::kPrefetch ? BLKW : 1];
+        bool nxt_full[NCH];
+        uint32_t words[NCH][BLK / 32];
+        bool split_fast = false;
+        if constexpr ((CFG::kAbl & kAblFullBlocks) != 0) {
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                const uint4* p = reinterpret_cast<const uint4*>(a.data + start[c] + (uint64_t)BLK * blk);
+#pragma unroll
+                for (int i = 0; i < BLKW / 4; i++) {
+                    const uint4 v = p[i];
+                    cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
+                }
+            }
+            block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 7) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg,
+                                                                             tab, a);
+            split_fast = true;
+        } else if constexpr (CFG::kAbl & 16) {
+            // split body: when every lane's block is whole, a branch of its own loads and
+            // scans it, so no control-flow merge sits between the loads and their uses (hipcc
+            // waits for all 16 loads at such a merge; here it waits per 64 bytes scanned).
+            // Interleaved A/B: 1.59 -> 1.52 ms per 4 GiB (profiles/r01/probes/scan_split_body_ab.jsonl)
+            bool full = true;
+#pragma unroll
+            for (int c = 0; c < NCH; c++)
+                full = full && blk < nblk[c] && start[c] + (uint64_t)BLK * (blk + 1) <= end[c];
+            split_fast = __all(full);
+            if (split_fast) {
+#pragma unroll
+                for (int c = 0; c < NCH; c++) {
+                    const uint4* p = reinterpret_cast<const uint4*>(a.data + start[c] + (uint64_t)BLK * blk);
+#pragma unroll
+                    for (int i = 0; i < BLKW / 4; i++) {
+                        const uint4 v = p[i];
+                        cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
+                    }
+                }
+                block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 3) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg,
+                                                                                 tab, a);
+            }
+        }
+        if (!split_fast) {
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            if constexpr (CFG::kPrefetch) {
+                fix_block<BLKW>(cur[c], cur_full[c], a.data, start[c] + (uint64_t)BLK * blk, end[c]);
+                const bool act = blk + 1 < nblk[c];
+                nxt_full[c] = load_block_nb<BLKW>(nxt[c], a.data, a.zero_page,
+                                                  act ? start[c] + (uint64_t)BLK * (blk + 1) : 0, act ? end[c] : 0);
+            } else if constexpr (CFG::kAbl & 8) {
+#pragma unroll
+                for (int i = 0; i < BLKW; i++) cur[c][i] = prev[c][i & 15] * 0x9E3779B1u + blk;
+            } else {
+                const bool act = blk < nblk[c];
+                load_block<BLKW>(cur[c], a.data, act ? start[c] + (uint64_t)BLK * blk : 0, act ? end[c] : 0);
+            }
+        }
+        block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 15) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg, tab, a);
+        }
+        if constexpr (CFG::kFuse == 2) {
+            // candidates are rare (~1 per 4 KiB): a divergent, seldom-taken append
+#pragma unroll
+            for (int c = 0; c < NCH; c++)
+#pragma unroll
+                for (int w = 0; w < BLK / 32; w++) {
+                    uint32_t bits = blk < nblk[c] ? words[c][w] : 0u;
+                    while (bits) {
+                        const uint32_t off = blk * BLK + 32 * w + __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        if (start[c] + off < end[c]) sum_push(sm[c], ncand[c], off);
+                    }
+                }
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            if constexpr (CFG::kFuse == 2)
+                if (ncand[c] > kSumCands && ovf_off[c] == 0xFFFFFFFFu) ovf_off[c] = blk * BLK;
+            if (blk < nblk[c] && (!sparse_bm || ncand[c] > kSumCands)) {
+                const uint64_t pos = start[c] + (uint64_t)BLK * blk;
+                uint32_t* bm = a.bitmap + (pos >> 5);
+                if (pos + BLK <= end[c]) {
+                    if constexpr (BLK >= 128) {
+#pragma unroll
+                        for (int w = 0; w < BLK / 32; w += 4)
+                            *reinterpret_cast<uint4*>(bm + w) =
+                                make_uint4(words[c][w], words[c][w + 1], words[c][w + 2], words[c][w + 3]);
+                    } else {
+                        *reinterpret_cast<uint2*>(bm) = make_uint2(words[c][0], words[c][1]);
+                    }
+                } else {
+                    // buffer tail: words past the buffer end may belong to the next buffer
+#pragma unroll
+                    for (int w = 0; w < BLK / 32; w++)
+                        if (pos + 32 * w < end[c]) bm[w] = words[c][w];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 16; i++) prev[c][i] = cur[c][BLKW - 16 + i];
+            if constexpr (CFG::kPrefetch) {
+#pragma unroll
+                for (int i = 0; i < BLKW; i++) cur[c][i] = nxt[c][i];
+                cur_full[c] = nxt_full[c];
+            }
+        }
+    }
+    if constexpr (CFG::kFuse != 0) {
+        if (a.fuse_resolve) {
+            // this wave's 64 segments are buffer seg0 / 64: make the lanes' bitmap stores
+            // visible to the whole wave (same CU, so no L1 staleness), then walk its cuts
+            const uint64_t seg0 = base + (tid & ~63u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if constexpr (CFG::kFuse == 2) {
+#pragma unroll
+                for (int c = 0; c < NCH; c++) {
+                    const uint64_t sc = seg0 + (uint64_t)c * bdim;
+                    if (sc < total)
+                        resolve_from_summary<(CFG::kAbl & 128) == 0>(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c], ovf_off[c], a.seg_len,
+                                             lhist);
+                }
+            } else {
+                if (seg0 < total) resolve_buffer(a.res, (uint32_t)(seg0 >> 6), lane, lhist);
+            }
+        }
+    }
+}
+
 template <int W, int PK, class CFG>
 __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
     static_assert(!CFG::kMirror || !CFG::kPrefetch, "mirrored state: no prefetch");
     static_assert(CFG::kMirror || PK != 2, "the one-compare predicate needs the mirrored state");
-    constexpr int MB =
-        (CFG::kMirror ? kAblMirror : 0) | (CFG::kAbl & (kAblSgprPred | kAblSdwa | kAblSdwaPop | kAblMinGroup | kAblMinGroup8 | kAblPopSwap));
     constexpr int NCH = CFG::kChains;
     constexpr int C = CFG::kCopies;
-    constexpr int BLK = CFG::kBlk;
-    constexpr int BLKW = BLK / 4;
     __shared__ __attribute__((aligned(16))) uint8_t tab[CFG::kLds];
     __shared__ uint32_t lhist[CFG::kFuse ? kMaxBins : 1];  // fused resolve: chunk-length histogram
     {
@@ -676,205 +893,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
     const uint64_t per_iter = (uint64_t)blockDim.x * NCH;
 
     for (uint64_t base = (uint64_t)blockIdx.x * per_iter; base < total; base += (uint64_t)gridDim.x * per_iter) {
-        uint64_t start[NCH], end[NCH];
-        uint32_t nblk[NCH];
-        bool first[NCH];
-        uint32_t maxblk = 0;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            const uint64_t seg = base + (uint64_t)c * blockDim.x + threadIdx.x;
-            start[c] = end[c] = 0;
-            nblk[c] = 0;
-            first[c] = true;
-            if (seg < total) {
-                uint64_t bstart, blen, sidx;
-                if (a.uniform_len) {
-                    const uint64_t spb = (a.uniform_len + a.seg_len - 1) / a.seg_len;
-                    const uint64_t b = seg / spb;
-                    sidx = seg - b * spb;
-                    bstart = b * a.uniform_len;
-                    blen = a.uniform_len;
-                } else {
-                    uint32_t lo_b = 0, hi_b = a.nbuf;  // last b with seg_prefix[b] <= seg
-                    while (hi_b - lo_b > 1) {
-                        const uint32_t mid = (lo_b + hi_b) >> 1;
-                        if (a.seg_prefix[mid] <= seg) lo_b = mid; else hi_b = mid;
-                    }
-                    sidx = seg - a.seg_prefix[lo_b];
-                    bstart = a.offs[lo_b];
-                    blen = a.lens[lo_b];
-                }
-                start[c] = bstart + sidx * a.seg_len;
-                const uint64_t bend = bstart + blen;
-                end[c] = start[c] + a.seg_len < bend ? start[c] + a.seg_len : bend;
-                nblk[c] = (uint32_t)((end[c] - start[c] + BLK - 1) / BLK);
-                // window warm-up reads the previous 64 bytes unless this is the buffer's first segment
-                first[c] = start[c] == bstart;
-            }
-            maxblk = nblk[c] > maxblk ? nblk[c] : maxblk;
-        }
-
-        uint32_t lo[NCH], hi[NCH];
-        uint32_t prev[NCH][16], cur[NCH][BLKW];
-        bool cur_full[NCH];
-        uint32_t sm[NCH][4];  // FUSE == 2: candidate summary per chain
-        uint32_t ncand[NCH];
-        uint32_t ovf_off[NCH];  // FUSE == 2: segment offset of the first stored bitmap block
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            sm[c][0] = sm[c][1] = sm[c][2] = sm[c][3] = 0xFFFFFFFFu;
-            ncand[c] = 0;
-            ovf_off[c] = 0xFFFFFFFFu;
-        }
-        // FUSE == 2 with the fused resolve: bitmap words are stored only once a lane's summary has
-        // overflowed (> kSumCands candidates), from that block on; resolve_from_summary reads them
-        // only there.  Saves the 0.5 GB of bitmap writes per 4 GiB.
-        const bool sparse_bm = CFG::kFuse == 2 && a.fuse_resolve;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            if (nblk[c] != 0 && !first[c]) {
-                load_block<16>(prev[c], a.data, start[c] - 64, start[c]);
-                if constexpr (CFG::kMirror)
-#pragma unroll
-                    for (int i = 0; i < 16; i++) prev[c][i] = __builtin_bitreverse32(prev[c][i]);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 16; i++) prev[c][i] = 0;  // bytes before the buffer are empty
-            }
-            lo[c] = hi[c] = 0;
-            warm_from<W, 64 - W, CFG::kMirror>(lo[c], hi[c], prev[c], push_base, a.jshift, tab);
-            if constexpr (CFG::kPrefetch) {
-                const bool act = nblk[c] != 0;
-                cur_full[c] = load_block_nb<BLKW>(cur[c], a.data, a.zero_page, act ? start[c] : 0, act ? end[c] : 0);
-            }
-        }
-
-        for (uint32_t blk = 0; blk < maxblk; blk++) {
-            uint32_t nxt[NCH][CFG::kPrefetch ? BLKW : 1];
-            bool nxt_full[NCH];
-            uint32_t words[NCH][BLK / 32];
-            bool split_fast = false;
-            if constexpr ((CFG::kAbl & kAblFullBlocks) != 0) {
-#pragma unroll
-                for (int c = 0; c < NCH; c++) {
-                    const uint4* p = reinterpret_cast<const uint4*>(a.data + start[c] + (uint64_t)BLK * blk);
-#pragma unroll
-                    for (int i = 0; i < BLKW / 4; i++) {
-                        const uint4 v = p[i];
-                        cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
-                    }
-                }
-                block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 7) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg,
-                                                                                 tab, a);
-                split_fast = true;
-            } else if constexpr (CFG::kAbl & 16) {
-                // split body: when every lane's block is whole, a branch of its own loads and
-                // scans it, so no control-flow merge sits between the loads and their uses (hipcc
-                // waits for all 16 loads at such a merge; here it waits per 64 bytes scanned).
-                // Interleaved A/B: 1.59 -> 1.52 ms per 4 GiB (profiles/r01/probes/scan_split_body_ab.jsonl)
-                bool full = true;
-#pragma unroll
-                for (int c = 0; c < NCH; c++)
-                    full = full && blk < nblk[c] && start[c] + (uint64_t)BLK * (blk + 1) <= end[c];
-                split_fast = __all(full);
-                if (split_fast) {
-#pragma unroll
-                    for (int c = 0; c < NCH; c++) {
-                        const uint4* p = reinterpret_cast<const uint4*>(a.data + start[c] + (uint64_t)BLK * blk);
-#pragma unroll
-                        for (int i = 0; i < BLKW / 4; i++) {
-                            const uint4 v = p[i];
-                            cur[c][4 * i] = v.x; cur[c][4 * i + 1] = v.y; cur[c][4 * i + 2] = v.z; cur[c][4 * i + 3] = v.w;
-                        }
-                    }
-                    block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 3) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg,
-                                                                                     tab, a);
-                }
-            }
-            if (!split_fast) {
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                if constexpr (CFG::kPrefetch) {
-                    fix_block<BLKW>(cur[c], cur_full[c], a.data, start[c] + (uint64_t)BLK * blk, end[c]);
-                    const bool act = blk + 1 < nblk[c];
-                    nxt_full[c] = load_block_nb<BLKW>(nxt[c], a.data, a.zero_page,
-                                                      act ? start[c] + (uint64_t)BLK * (blk + 1) : 0, act ? end[c] : 0);
-                } else if constexpr (CFG::kAbl & 8) {
-#pragma unroll
-                    for (int i = 0; i < BLKW; i++) cur[c][i] = prev[c][i & 15] * 0x9E3779B1u + blk;
-                } else {
-                    const bool act = blk < nblk[c];
-                    load_block<BLKW>(cur[c], a.data, act ? start[c] + (uint64_t)BLK * blk : 0, act ? end[c] : 0);
-                }
-            }
-            block_words<W, PK, 0, BLK / 32, NCH, (CFG::kAbl & 15) | MB, BLKW>(words, lo, hi, cur, prev, qa_reg, pa_reg, tab, a);
-            }
-            if constexpr (CFG::kFuse == 2) {
-                // candidates are rare (~1 per 4 KiB): a divergent, seldom-taken append
-#pragma unroll
-                for (int c = 0; c < NCH; c++)
-#pragma unroll
-                    for (int w = 0; w < BLK / 32; w++) {
-                        uint32_t bits = blk < nblk[c] ? words[c][w] : 0u;
-                        while (bits) {
-                            const uint32_t off = blk * BLK + 32 * w + __builtin_ctz(bits);
-                            bits &= bits - 1;
-                            if (start[c] + off < end[c]) sum_push(sm[c], ncand[c], off);
-                        }
-                    }
-            }
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                if constexpr (CFG::kFuse == 2)
-                    if (ncand[c] > kSumCands && ovf_off[c] == 0xFFFFFFFFu) ovf_off[c] = blk * BLK;
-                if (blk < nblk[c] && (!sparse_bm || ncand[c] > kSumCands)) {
-                    const uint64_t pos = start[c] + (uint64_t)BLK * blk;
-                    uint32_t* bm = a.bitmap + (pos >> 5);
-                    if (pos + BLK <= end[c]) {
-                        if constexpr (BLK >= 128) {
-#pragma unroll
-                            for (int w = 0; w < BLK / 32; w += 4)
-                                *reinterpret_cast<uint4*>(bm + w) =
-                                    make_uint4(words[c][w], words[c][w + 1], words[c][w + 2], words[c][w + 3]);
-                        } else {
-                            *reinterpret_cast<uint2*>(bm) = make_uint2(words[c][0], words[c][1]);
-                        }
-                    } else {
-                        // buffer tail: words past the buffer end may belong to the next buffer
-#pragma unroll
-                        for (int w = 0; w < BLK / 32; w++)
-                            if (pos + 32 * w < end[c]) bm[w] = words[c][w];
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < 16; i++) prev[c][i] = cur[c][BLKW - 16 + i];
-                if constexpr (CFG::kPrefetch) {
-#pragma unroll
-                    for (int i = 0; i < BLKW; i++) cur[c][i] = nxt[c][i];
-                    cur_full[c] = nxt_full[c];
-                }
-            }
-        }
-        if constexpr (CFG::kFuse != 0) {
-            if (a.fuse_resolve) {
-                // this wave's 64 segments are buffer seg0 / 64: make the lanes' bitmap stores
-                // visible to the whole wave (same CU, so no L1 staleness), then walk its cuts
-                const uint64_t seg0 = base + (threadIdx.x & ~63u);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                if constexpr (CFG::kFuse == 2) {
-#pragma unroll
-                    for (int c = 0; c < NCH; c++) {
-                        const uint64_t sc = seg0 + (uint64_t)c * blockDim.x;
-                        if (sc < total)
-                            resolve_from_summary<(CFG::kAbl & 128) == 0>(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c], ovf_off[c], a.seg_len,
-                                                 lhist);
-                    }
-                } else {
-                    if (seg0 < total) resolve_buffer(a.res, (uint32_t)(seg0 >> 6), lane, lhist);
-                }
-            }
-        }
+        scan_iter<W, PK, CFG>(a, tab, lhist, base, threadIdx.x, blockDim.x, total, lane, c8, push_base, pa_reg, qa_reg);
     }
     if constexpr (CFG::kFuse != 0) {
         if (a.fuse_resolve) {
@@ -1204,6 +1223,78 @@ __global__ __launch_bounds__(256) void chunk_hash_persistent_kernel(HashArgs a) 
         if (base >= total) break;
         if (base + lane < total) hash_task<ALGO, ABL, PF>(a, base + lane);
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// 5a. scan and fingerprint of two different batches in ONE persistent kernel (round 3)
+//     The scan is latency-bound (its waves wait on the LDS-read chain half the time, VALU ~60 %
+//     busy) and the fingerprint issue-bound (VALU ~75 %, waves waiting for issue slots): run on
+//     the same SIMDs they fill each other's gaps, which two kernels on two streams do not do —
+//     whole-CU scan workgroups and the fingerprint kernel's VGPRs keep them on separate CUs.
+//     Each wave takes work items from two queues: a scan item is one whole write buffer (64
+//     segments, the fused cut walk included), a fingerprint item is 64 consecutive tasks of the
+//     OTHER (previous) batch's longest-first task list.  Waves 4k..4k+3 of a workgroup sit on the
+//     four SIMDs; waves with bit 2 of their index clear prefer the scan queue, the others the
+//     fingerprint queue, and a wave whose queue is empty takes from the other, so both kinds
+//     share every SIMD until one queue runs dry.  ctr[0] / ctr[1]: zeroed item counters.
+//     Uniform batches whose buffers are exactly 64 segments (the fused cut walk) only.
+// ------------------------------------------------------------------------------------------
+template <int W, int PK, class CFG, int ALGO>
+__global__ __launch_bounds__(1024, 1) void cdc_fused_kernel(ScanArgs a, HashArgs ha, uint32_t* ctr) {
+    static_assert(CFG::kFuse == 2 && CFG::kChains == 1, "fused form: one chain, register-summary cut walk");
+    constexpr int C = CFG::kCopies;
+    __shared__ __attribute__((aligned(16))) uint8_t tab[CFG::kLds];
+    __shared__ uint32_t lhist[kMaxBins];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.tab_image);
+        uint4* dst = reinterpret_cast<uint4*>(tab);
+        for (int i = threadIdx.x; i < CFG::kLds / 16; i += blockDim.x) dst[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < kMaxBins; i += blockDim.x) lhist[i] = 0;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c8 = (lane & (C - 1)) << 3;
+    const uint32_t push_base = CFG::kPushOff | c8;
+    uint32_t pa_reg = push_base, qa_reg = c8;
+    const uint64_t total = a.total_segs;
+    const uint32_t nscan = a.fuse_resolve ? (uint32_t)(total >> 6) : 0u;
+    const uint32_t htotal = ha.total ? *ha.total : 0u;
+    const bool scan_first = ((threadIdx.x >> 8) & 1) == 0;
+    bool scan_left = nscan != 0, hash_left = htotal != 0;
+    while (scan_left || hash_left) {
+        const bool do_scan = scan_left && (scan_first || !hash_left);
+        uint32_t it = 0;
+        if (lane == 0) it = atomicAdd(&ctr[do_scan ? 0 : 1], 1u);
+        it = __builtin_amdgcn_readfirstlane(__shfl(it, 0));
+        if (do_scan) {
+            if (it >= nscan) {
+                scan_left = false;
+                continue;
+            }
+            scan_iter<W, PK, CFG>(a, tab, lhist, (uint64_t)it * 64, lane, 64, total, lane, c8, push_base, pa_reg, qa_reg);
+        } else {
+            const uint32_t i0 = it * 64;
+            if (i0 >= htotal) {
+                hash_left = false;
+                continue;
+            }
+            // issue priority for waves of long chunks, as in chunk_hash_kernel (task i0 is the
+            // wave's longest: the list is longest-first)
+            const uint32_t nb = __builtin_amdgcn_readfirstlane(sha_blocks(ha.clens[ha.tasks[i0]]));
+            if (nb > 1024)
+                __builtin_amdgcn_s_setprio(3);
+            else if (nb > 512)
+                __builtin_amdgcn_s_setprio(2);
+            else if (nb > 256)
+                __builtin_amdgcn_s_setprio(1);
+            if (i0 + lane < htotal) hash_task<ALGO, 16, true>(ha, i0 + lane);
+            __builtin_amdgcn_s_setprio(0);
+        }
+    }
+    __syncthreads();
+    if (nscan)
+        for (uint32_t i = threadIdx.x; i < a.res.nbins; i += blockDim.x)
+            if (lhist[i]) atomicAdd(&a.res.hist[i], lhist[i]);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -185,6 +185,10 @@ ScanVariantInfo scan_variant_info_sweep(int variant);
 ScanVariantInfo scan_variant_info_sweep_r3(int variant);
 hipError_t launch_scan_sweep_r3(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
                                 hipStream_t s);
+// measurement probe (tuning build, SDFS_FUSED_PROBE): the fused scan + fingerprint kernel over the
+// batch's own scan (again: same slots, same values) and its fingerprint tasks
+hipError_t launch_fused_probe(const ScanArgs& a, const HashArgs& ha, uint32_t* ctr, int window, int pk, int grid,
+                              hipStream_t s);
 hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
                              hipStream_t stream);
 hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);

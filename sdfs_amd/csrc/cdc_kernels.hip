@@ -35,7 +35,15 @@ namespace sdfs {
 // one dependent instruction less in the rolling chain), the pop address one v_mov_b32_sdwa
 // instead of v_perm.  Interleaved A/B, identical records: 1.368 -> 1.245 ms per 4 GiB at the
 // 4 KiB-mean mix, 1.282 -> 1.162 at the reference default (sweep variant 32 = the form before).
-using ScanProd = ScanCfg<32, 1, false, 4, 16 | kAblSgprPred | kAblSdwa | kAblSdwaPop, 256, 2, kScanThreads, true>;
+// Also since round 3: the candidate bits of the one-compare predicate come from each 8-position
+// group's minimum predicate word (kAblMinGroup8: three v_min3 + one v_min + one compare per group,
+// exact bits only in groups where some lane has a candidate) instead of a per-position compare
+// into an SGPR pair and a scalar OR chain, and the pop entries are stored high word first
+// (kAblPopSwap) so the low-word xor3 never reads three registers of one bank.  Interleaved A/B,
+// identical records: 1.258 -> 1.235 ms (4 KiB-mean mix), 1.157 -> 1.134 (default), sweep
+// variant 51 = this form, 44 = the SDWA form before it.
+using ScanProd = ScanCfg<32, 1, false, 4, 16 | kAblSdwa | kAblSdwaPop | kAblMinGroup | kAblMinGroup8 | kAblPopSwap, 256,
+                         2, kScanThreads, true>;
 
 template <class CFG>
 constexpr ScanVariantInfo info_of() {

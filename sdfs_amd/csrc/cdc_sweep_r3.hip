@@ -28,6 +28,10 @@ using ScanV49 = ScanCfg<32, 1, false, 4, kProdR3 | kAblMinGroup | kAblMinGroup8,
 // bank conflict in the low-word xor3); 51: 50 with the groups-of-8 minimum candidate bits (49)
 using ScanV50 = ScanCfg<32, 1, false, 4, kProdR3 | kAblSgprPred | kAblPopSwap, 256, 2, kScanThreads, true>;
 using ScanV51 = ScanCfg<32, 1, false, 4, kProdR3 | kAblMinGroup | kAblMinGroup8 | kAblPopSwap, 256, 2, kScanThreads, true>;
+// 52: 51 with the bit-select pop address for the byte already in place (kAblPopMux); 53: 50 + mux
+using ScanV52 = ScanCfg<32, 1, false, 4, kProdR3 | kAblMinGroup | kAblMinGroup8 | kAblPopSwap | kAblPopMux, 256, 2,
+                        kScanThreads, true>;
+using ScanV53 = ScanCfg<32, 1, false, 4, kProdR3 | kAblSgprPred | kAblPopSwap | kAblPopMux, 256, 2, kScanThreads, true>;
 
 template <class CFG>
 constexpr ScanVariantInfo info_r3() {
@@ -46,6 +50,8 @@ ScanVariantInfo scan_variant_info_sweep_r3(int v) {
     case 49: return info_r3<ScanV49>();
     case 50: return info_r3<ScanV50>();
     case 51: return info_r3<ScanV51>();
+    case 52: return info_r3<ScanV52>();
+    case 53: return info_r3<ScanV53>();
     default: return {0, 0, 0, 0, 0, 0, 0, 0};
     }
 }
@@ -72,8 +78,21 @@ hipError_t launch_scan_sweep_r3(const ScanArgs& a, int window, int pk, int varia
     case 49: return launch_r3<ScanV49>(a, pk, grid, block, s);
     case 50: return launch_r3<ScanV50>(a, pk, grid, block, s);
     case 51: return launch_r3<ScanV51>(a, pk, grid, block, s);
+    case 52: return launch_r3<ScanV52>(a, pk, grid, block, s);
+    case 53: return launch_r3<ScanV53>(a, pk, grid, block, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_fused_probe(const ScanArgs& a, const HashArgs& ha, uint32_t* ctr, int window, int pk, int grid,
+                              hipStream_t s) {
+    using Prod = ScanV51;  // the production scan form
+    if (window != 48 || pk != 2 || !a.uniform_len || !a.fuse_resolve) return hipErrorInvalidValue;
+    if (ha.algo == 2)
+        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 2>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
+    else
+        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 0>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
+    return hipGetLastError();
 }
 
 }  // namespace sdfs

@@ -602,7 +602,10 @@ for mask, min_len in PRMS:
     p = O.Params(min_len=min_len, pred_mask=mask)
     exp[mask] = ([[O.chunk(h[b].tobytes(), p) for b in range(nbuf)] for h in (dense, rnd)],
                  [O.chunk(rb[int(ro[b]): int(ro[b]) + n].tobytes(), p) for b, n in enumerate(rl)])
-for variant in (0, 29, 30, 31, 32):
+VARIANTS = [int(v) for v in os.environ.get("SCAN_VARIANTS", "0,29,30,31,32").split(",")]
+if os.environ.get("LOWK_ONLY") == "1":  # round-3 sweep forms: the one-compare predicate only
+    PRMS = tuple(p for p in PRMS if (p[0] & (p[0] + 1)) == 0)
+for variant in VARIANTS:
     os.environ["SDFS_SCAN_VARIANT"] = str(variant)  # read at create (tuning library only)
     for mask, min_len in PRMS:
         cfg = SdfsConfig(min_len=min_len, pred_mask=mask)
@@ -629,6 +632,29 @@ for variant in (0, 29, 30, 31, 32):
         e.destroy()
 print("scan variants ok")
 """
+
+
+def _run_scan_variant_check(variants, lowk_only=False):
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ROOT=root, SDFS_CDC_LIB=_lib.TUNING_LIB, SCAN_VARIANTS=",".join(map(str, variants)),
+               LOWK_ONLY="1" if lowk_only else "0")
+    r = subprocess.run([sys.executable, "-c", _SCAN_VARIANT_CHECK], capture_output=True, text=True, env=env,
+                       timeout=110, cwd=root)
+    assert r.returncode == 0 and "scan variants ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_scan_variants_round3_agree():
+    """Round-3 scan forms (cdc_sweep_r3.hip): SDWA push address (43), SDWA push +
+    pop addresses (44), 16 table copies at 6 / 5 waves per SIMD (46 / 47), group-minimum candidate
+    bits in groups of 4 / 8 (48 / 49), pop entries high word first (50), 49 + 50 (51), + the
+    bit-select pop address (52), 50 + that (53) — the same oracle checks at the low-k-bit zero
+    predicates (12, 11, 13 bits), the only ones those forms are built for."""
+    _run_scan_variant_check([43, 44, 46, 47, 48, 49], lowk_only=True)
+    _run_scan_variant_check([50, 51, 52, 53], lowk_only=True)
 
 
 def test_scan_variants_agree():
