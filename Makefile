@@ -27,19 +27,19 @@ build/tuning/%.o: $(CSRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DSDFS_TUNING -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -ldl
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-z,defs -o $@ $(OBJS) -ldl
 
 $(TUNING_LIB): $(TUNING_OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(TUNING_OBJS) -ldl
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-z,defs -o $@ $(TUNING_OBJS) -ldl
 
 # host-side harnesses: the multi-threaded getChunks driver (bench.py, GPU tests) and the JNI glue
 tools: tools/libsdfs_threads.so jni/libsdfs_cdc_jni.so tests/jni/libjni_stub.so
 
 tools/libsdfs_threads.so: tools/threads_bench.c include/sdfs_cdc.h $(LIB)
-	gcc -O2 -std=c11 -fPIC -shared -Wall -Wextra -D_GNU_SOURCE -o $@ $< -Lsdfs_amd -lsdfs_cdc -Wl,-rpath,'$$ORIGIN/../sdfs_amd' -lpthread
+	gcc -O2 -std=c11 -fPIC -shared -Wl,-z,defs -Wall -Wextra -D_GNU_SOURCE -o $@ $< -Lsdfs_amd -lsdfs_cdc -Wl,-rpath,'$$ORIGIN/../sdfs_amd' -lpthread
 
 jni/libsdfs_cdc_jni.so: jni/sdfs_cdc_jni.c jni/jni_min.h include/sdfs_cdc.h $(LIB)
-	gcc -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ $< -Lsdfs_amd -lsdfs_cdc -Wl,-rpath,'$$ORIGIN/../sdfs_amd'
+	gcc -O2 -std=c11 -fPIC -shared -Wl,-z,defs -Wall -Wextra -o $@ $< -Lsdfs_amd -lsdfs_cdc -Wl,-rpath,'$$ORIGIN/../sdfs_amd'
 
 # test infrastructure: a stand-in JNIEnv for driving the JNI glue without a JVM (tests/test_jni.py)
 tests/jni/libjni_stub.so: tests/jni/jni_stub.c jni/jni_min.h
