@@ -176,7 +176,8 @@ int sdfs_cdc_get_chunks_stream(sdfs_cdc_engine* e, uint64_t stream_key, const ui
 /* The same with the caller writing the buffer's bytes itself: fill(ctx, dst, len) is called once,
  * on the calling thread, with dst = the space reserved for this call in the engine's pinned
  * staging (so a JNI caller copies its byte[] once, GetByteArrayRegion straight into it).  A
- * non-zero return from fill is returned by the call (its results are discarded). */
+ * non-zero return from fill fails the call with SDFS_CDC_EINVAL and sdfs_cdc_last_error()
+ * "getChunks: fill callback failed (<rc>)"; *count is 0 and no results are written. */
 typedef int (*sdfs_cdc_fill_fn)(void* ctx, uint8_t* dst, uint32_t len);
 int sdfs_cdc_get_chunks_fill(sdfs_cdc_engine* e, uint64_t stream_key, uint32_t len, sdfs_cdc_fill_fn fill, void* ctx,
                              uint32_t* starts, uint32_t* lens, uint8_t* digests, uint32_t cap, uint32_t* count);

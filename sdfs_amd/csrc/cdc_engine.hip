@@ -1540,6 +1540,28 @@ struct Coll {
         if (_r != 0) return fail(SDFS_CDC_EHIP, "%s failed: %s", #expr, (api)->errstr(_r));          \
     } while (0)
 
+// One all-gather per device of the set inside one RCCL group.  ncclGroupEnd runs on every path
+// once ncclGroupStart succeeded, so a failing device never leaves the group open on this thread.
+template <class Issue>
+int grouped_all_gather(const RcclApi* api, Set& s, Issue&& issue) {
+    const int g = api->group_start();
+    if (g) return fail(SDFS_CDC_EHIP, "ncclGroupStart failed: %s", api->errstr(g));
+    int rc = SDFS_CDC_OK;
+    for (int i = 0; i < (int)s.ndev() && rc == SDFS_CDC_OK; i++) {
+        const hipError_t he = hipSetDevice(s.ordinals[i]);
+        if (he != hipSuccess) {
+            rc = fail(SDFS_CDC_EHIP, "hipSetDevice(%d) failed: %s", s.ordinals[i], hipGetErrorString(he));
+            break;
+        }
+        const int r = issue(i);
+        if (r) rc = fail(SDFS_CDC_EHIP, "ncclAllGather on device %d failed: %s", s.ordinals[i], api->errstr(r));
+    }
+    const int e = api->group_end();
+    if (rc) return rc;
+    if (e) return fail(SDFS_CDC_EHIP, "ncclGroupEnd failed: %s", api->errstr(e));
+    return SDFS_CDC_OK;
+}
+
 int coll_ready(Set& s, Coll** out) {
     std::lock_guard<std::mutex> lk(s.coll_mu);
     if (s.coll) {
@@ -1598,7 +1620,7 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
     std::vector<int> ords;
     rc = device_set(p, &ords);
     if (rc) return rc;
-    H* h = nullptr;
+    void* h = nullptr;
     rc = reg().create(share_key(p, ords), ords,
                       [p](int ord, std::unique_ptr<DevEngine>* d) { return dev_create(p, ord, d); }, &h);
     if (rc) return rc;
@@ -1608,7 +1630,7 @@ int sdfs_cdc_create(const sdfs_cdc_params* p, sdfs_cdc_engine** out) {
 
 int sdfs_cdc_destroy(sdfs_cdc_engine* e) {
     if (!e) return SDFS_CDC_OK;
-    if (!reg().destroy(reinterpret_cast<H*>(e))) return fail(SDFS_CDC_EINVAL, "not a live engine handle");
+    if (!reg().destroy(e)) return fail(SDFS_CDC_EINVAL, "not a live engine handle");
     return SDFS_CDC_OK;
 }
 
@@ -1711,29 +1733,20 @@ int sdfs_cdc_get_chunks_batch(sdfs_cdc_engine* e, const uint8_t* base, const uin
     // Contiguous shares of the buffers, one per device, run concurrently (every buffer is chunked
     // from fresh state, so a share is an independent batch); at least kShareMin buffers per device.
     constexpr uint32_t kShareMin = 64;
-    const uint32_t k = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(s.ndev(), nbuf / kShareMin));
-    if (k == 1) {
-        const size_t i = Reg::pick(s, false, 0);
-        Reg::Load ld(s, i);
-        return dev_get_chunks_batch(s.devs[i].get(), base, offs, lens, nbuf, counts, starts, lens_out, digests, cap);
-    }
     const uint32_t dl = s.devs[0]->digest_len;
-    std::vector<int> rcs(k, 0);
-    std::vector<std::string> errs(k);
-    auto share = [&](uint32_t d) {
-        Reg::Load ld(s, d);
-        const uint32_t b0 = share_begin(nbuf, k, d), b1 = share_begin(nbuf, k, d + 1);
-        const uint64_t o = (uint64_t)b0 * cap;
-        rcs[d] = dev_get_chunks_batch(s.devs[d].get(), base, offs + b0, lens + b0, b1 - b0, counts + b0, starts + o,
-                                      lens_out + o, digests ? digests + o * dl : nullptr, cap);
-        if (rcs[d]) errs[d] = g_last_error;
-    };
-    std::vector<std::thread> th;
-    for (uint32_t d = 1; d < k; d++) th.emplace_back(share, d);
-    share(0);
-    for (auto& t : th) t.join();
-    for (uint32_t d = 0; d < k; d++)
-        if (rcs[d]) return fail(rcs[d], "device %d: %s", s.ordinals[d], errs[d].c_str());
+    std::vector<std::string> errs(s.ndev());
+    size_t bad = 0;
+    const int rc = Reg::run_shares(
+        s, nbuf, kShareMin,
+        [&](size_t d, uint32_t b0, uint32_t b1) {
+            const uint64_t o = (uint64_t)b0 * cap;
+            const int r = dev_get_chunks_batch(s.devs[d].get(), base, offs + b0, lens + b0, b1 - b0, counts + b0,
+                                               starts + o, lens_out + o, digests ? digests + o * dl : nullptr, cap);
+            if (r) errs[d] = g_last_error;  // per-thread message, kept for the caller's thread
+            return r;
+        },
+        &bad);
+    if (rc) return fail(rc, "device %d: %s", s.ordinals[bad], errs[bad].c_str());
     return SDFS_CDC_OK;
 }
 
@@ -1747,8 +1760,21 @@ int sdfs_cdc_get_chunks_fill(sdfs_cdc_engine* e, uint64_t stream_key, uint32_t l
     Set& s = u.set();
     const size_t i = Reg::pick(s, stream_key != SDFS_CDC_NO_STREAM, stream_key);
     Reg::Load ld(s, i);
-    return dev_get_chunks(
-        s.devs[i].get(), len, [&](uint8_t* dst) { return fill(ctx, dst, len); }, starts, lens, digests, cap, count);
+    int frc = 0;
+    const int rc = dev_get_chunks(
+        s.devs[i].get(), len,
+        [&](uint8_t* dst) {
+            frc = fill(ctx, dst, len);
+            if (!frc) return 0;
+            memset(dst, 0, len);  // the batch still scans this request's bytes: defined ones
+            return (int)SDFS_CDC_EINVAL;
+        },
+        starts, lens, digests, cap, count);
+    if (frc) {
+        *count = 0;
+        return fail(SDFS_CDC_EINVAL, "getChunks: fill callback failed (%d)", frc);
+    }
+    return rc;
 }
 
 static int copy_fill(void* ctx, uint8_t* dst, uint32_t len) {
@@ -1890,12 +1916,10 @@ int sdfs_cdc_allgather_records(sdfs_cdc_engine* e, uint8_t* const* records, cons
     auto st = [&](int i) { return streams ? reinterpret_cast<hipStream_t>(streams[i]) : (hipStream_t) nullptr; };
     std::lock_guard<std::mutex> lk(s.coll_mu);  // one exchange of the set at a time (shared count buffers)
     // 1. counts: one u32 per device, gathered on every device; device 0's copy to the host
-    NCCL_TRY(api, api->group_start());
-    for (int i = 0; i < n; i++) {
-        HIP_TRY(hipSetDevice(s.ordinals[i]));
-        NCCL_TRY(api, api->all_gather(d_totals[i], c->d_counts[i], 1, kNcclUint32, c->comms[i], st(i)));
-    }
-    NCCL_TRY(api, api->group_end());
+    rc = grouped_all_gather(api, s, [&](int i) {
+        return api->all_gather(d_totals[i], c->d_counts[i], 1, kNcclUint32, c->comms[i], st(i));
+    });
+    if (rc) return rc;
     HIP_TRY(hipSetDevice(s.ordinals[0]));
     HIP_TRY(hipMemcpyAsync(c->h_counts, c->d_counts[0], 4ull * n, hipMemcpyDeviceToHost, st(0)));
     HIP_TRY(hipStreamSynchronize(st(0)));
@@ -1914,14 +1938,9 @@ int sdfs_cdc_allgather_records(sdfs_cdc_engine* e, uint8_t* const* records, cons
     *stride = m;
     if (m == 0) return SDFS_CDC_OK;
     // 2. the tables, padded to the largest count: device j's records at gathered[i] + j*m*48
-    NCCL_TRY(api, api->group_start());
-    for (int i = 0; i < n; i++) {
-        HIP_TRY(hipSetDevice(s.ordinals[i]));
-        NCCL_TRY(api, api->all_gather(records[i], gathered[i], m * SDFS_CDC_RECORD_BYTES, kNcclUint8, c->comms[i],
-                                      st(i)));
-    }
-    NCCL_TRY(api, api->group_end());
-    return SDFS_CDC_OK;
+    return grouped_all_gather(api, s, [&](int i) {
+        return api->all_gather(records[i], gathered[i], m * SDFS_CDC_RECORD_BYTES, kNcclUint8, c->comms[i], st(i));
+    });
 }
 
 }  // extern "C"

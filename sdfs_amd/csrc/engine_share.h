@@ -25,6 +25,7 @@
 // to the device with the fewest calls in progress (ties: round robin).
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -33,6 +34,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace sdfs {
@@ -55,7 +57,7 @@ struct SharedSet {
 template <class Dev>
 struct Handle {
     SharedSet<Dev>* set = nullptr;
-    std::atomic<int> inflight{0};
+    int inflight = 0;  // calls in progress (guarded by mu)
     std::mutex mu;
     std::condition_variable cv;  // inflight reached 0
 };
@@ -65,6 +67,13 @@ inline uint64_t share_mix64(uint64_t x) {  // splitmix64 finaliser: spreads stre
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
     return x ^ (x >> 31);
+}
+
+// Contiguous shares of n buffers over k devices (first n % k devices take one more):
+// device i gets [begin(i), begin(i+1)).
+inline uint32_t share_begin(uint32_t n, uint32_t k, uint32_t i) {
+    const uint32_t q = n / k, r = n % k;
+    return i * q + (i < r ? i : r);
 }
 
 template <class Dev>
@@ -77,7 +86,7 @@ class Registry {
     // make(ordinal, std::unique_ptr<Dev>*) -> status (0 = ok) for every ordinal.  Creation and
     // teardown are serialised among themselves, not against calls.
     template <class Make>
-    int create(const std::string& key, const std::vector<int>& ordinals, Make&& make, H** out) {
+    int create(const std::string& key, const std::vector<int>& ordinals, Make&& make, void** out) {
         *out = nullptr;
         std::lock_guard<std::mutex> life(life_mu_);
         {
@@ -112,15 +121,21 @@ class Registry {
     }
 
     // Ends a handle: no new calls, wait for the ones in progress, drop the reference (the last
-    // one tears the set down).  false: not a live handle.
-    bool destroy(H* h) {
+    // one tears the set down).  false: not a live handle (never issued, or already destroyed).
+    bool destroy(const void* tok) {
+        H* h = nullptr;
         {
             std::lock_guard<std::mutex> lk(mu_);
-            if (!live_.erase(h)) return false;
+            auto it = live_.find(reinterpret_cast<uintptr_t>(tok));
+            if (it == live_.end()) return false;
+            h = it->second;
+            live_.erase(it);  // no Use can start on h from here on
         }
         {
+            // Use::~Use decrements under h->mu and touches h no more after unlocking it, so once
+            // this wait returns nothing else can reach h
             std::unique_lock<std::mutex> lk(h->mu);
-            h->cv.wait(lk, [&] { return h->inflight.load() == 0; });
+            h->cv.wait(lk, [&] { return h->inflight == 0; });
         }
         std::lock_guard<std::mutex> life(life_mu_);
         S* dead = nullptr;
@@ -136,22 +151,22 @@ class Registry {
         return true;
     }
 
-    // A call in progress on a handle (RAII): ok() false when the handle is not live.
+    // A call in progress on a handle (RAII): ok() false when the token is not a live handle.
     class Use {
       public:
-        Use(Registry& r, const void* hp) {
+        Use(Registry& r, const void* tok) {
             std::lock_guard<std::mutex> lk(r.mu_);
-            auto it = r.live_.find(static_cast<H*>(const_cast<void*>(hp)));
+            auto it = r.live_.find(reinterpret_cast<uintptr_t>(tok));
             if (it == r.live_.end()) return;
-            h_ = *it;
+            h_ = it->second;
+            std::lock_guard<std::mutex> hl(h_->mu);
             h_->inflight++;
         }
         ~Use() {
             if (!h_) return;
-            if (--h_->inflight == 0) {
-                std::lock_guard<std::mutex> lk(h_->mu);  // orders the wake-up after destroy's check
-                h_->cv.notify_all();
-            }
+            std::lock_guard<std::mutex> lk(h_->mu);
+            if (--h_->inflight == 0) h_->cv.notify_all();
+            if (after_release_hook) after_release_hook();  // tests: widen the window before unlock
         }
         Use(const Use&) = delete;
         Use& operator=(const Use&) = delete;
@@ -161,6 +176,10 @@ class Registry {
       private:
         H* h_ = nullptr;
     };
+
+    // Test hook run by ~Use after its decrement, still holding the handle's lock (null in the
+    // product).
+    static inline void (*after_release_hook)() = nullptr;
 
     // Device for a host call: key mod N for keyed calls, else the least-loaded device.
     static size_t pick(S& s, bool keyed, uint64_t key) {
@@ -188,6 +207,46 @@ class Registry {
         std::atomic<int>& c_;
       };
 
+    // One batch of nbuf independent buffers over the set: contiguous shares, one per device, at
+    // least min_share buffers each, run concurrently (the calling thread takes share 0) as
+    // run(device index, first buffer, end buffer) -> status.  A batch too small to split goes
+    // whole to the least-loaded device.  Returns 0, or the first failing share's status with
+    // *failed set to its device index.
+    template <class Run>
+    static int run_shares(S& s, uint32_t nbuf, uint32_t min_share, Run&& run, size_t* failed) {
+        *failed = 0;
+        const uint64_t want = min_share ? nbuf / min_share : nbuf;
+        const uint32_t k = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(s.ndev(), want));
+        if (k == 1) {
+            const size_t i = pick(s, false, 0);
+            Load ld(s, i);
+            *failed = i;
+            return run(i, 0u, nbuf);
+        }
+        std::vector<int> rcs(k, 0);
+        auto share = [&](uint32_t d) {
+            Load ld(s, d);
+            rcs[d] = run((size_t)d, share_begin(nbuf, k, d), share_begin(nbuf, k, d + 1));
+        };
+        std::vector<std::thread> th;
+        for (uint32_t d = 1; d < k; d++) th.emplace_back(share, d);
+        share(0);
+        for (auto& t : th) t.join();
+        for (uint32_t d = 0; d < k; d++)
+            if (rcs[d]) {
+                *failed = d;
+                return rcs[d];
+            }
+        return 0;
+    }
+
+    // The set behind a live token (tests); null when the token is not live.
+    S* set_of(const void* tok) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = live_.find(reinterpret_cast<uintptr_t>(tok));
+        return it == live_.end() ? nullptr : it->second->set;
+    }
+
     // handles sharing a set (statistics, tests)
     int refs_of(const S& s) {
         std::lock_guard<std::mutex> lk(mu_);
@@ -203,24 +262,21 @@ class Registry {
     }
 
   private:
-    H* new_handle(S* s) {  // registry lock held
+    // Tokens are never reused (a 64-bit counter), so a stale token from a destroyed handle can
+    // never name a later handle: every call on it fails with EINVAL, a second destroy too.
+    void* new_handle(S* s) {  // registry lock held
         H* h = new H();
         h->set = s;
-        live_.insert(h);
-        return h;
+        const uintptr_t tok = (++next_tok_) << 4;  // nonzero, 16-byte "aligned" like a pointer
+        live_.emplace(tok, h);
+        return reinterpret_cast<void*>(tok);
     }
 
     std::mutex life_mu_;  // create / teardown
     std::mutex mu_;       // live handles, sets, reference counts
-    std::set<H*> live_;
+    uintptr_t next_tok_ = 0;
+    std::map<uintptr_t, H*> live_;
     std::map<std::string, S*> sets_;
 };
-
-// Contiguous shares of n buffers over k devices (first n % k devices take one more):
-// device i gets [begin(i), begin(i+1)).
-inline uint32_t share_begin(uint32_t n, uint32_t k, uint32_t i) {
-    const uint32_t q = n / k, r = n % k;
-    return i * q + (i < r ? i : r);
-}
 
 }  // namespace sdfs

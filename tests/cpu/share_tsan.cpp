@@ -13,7 +13,11 @@
 //   3. keyed calls always reach the same device (key -> device is a function), unkeyed calls
 //      spread over the set, contiguous shares partition a batch;
 //   4. queue shutdown with callers in flight: every caller gets its own correct result or
-//      kQueueStopped, nobody hangs.
+//      kQueueStopped, nobody hangs;
+//   5. a call releasing its handle while destroy runs: destroy waits for the release to finish;
+//      handle tokens are never reused;
+//   6. the batch split of sdfs_cdc_get_chunks_batch at 2 and 8 devices processes every buffer
+//      exactly once, and stream-key routing is stable.
 // Test infrastructure only.
 #include <algorithm>
 #include <atomic>
@@ -21,6 +25,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <mutex>
+#include <string>
 #include <random>
 #include <thread>
 #include <vector>
@@ -124,12 +130,13 @@ static int sharing_and_lifecycle() {
     g_built = 0;
     g_torn = 0;
     Reg reg;
-    Handle<FakeDev>*a, *b, *c;
+    void *a, *b, *c;
     if (reg.create("K1", {0, 1, 2}, make, &a) || reg.create("K1", {0, 1, 2}, make, &b) ||
         reg.create("K2", {0}, make, &c))
         return 10;
-    if (a->set != b->set || a->set == c->set || reg.sets() != 2 || reg.handles() != 3) return 11;
-    if (reg.refs_of(*a->set) != 2 || g_built != 4) return 12;
+    if (reg.set_of(a) != reg.set_of(b) || reg.set_of(a) == reg.set_of(c) || reg.sets() != 2 || reg.handles() != 3)
+        return 11;
+    if (reg.refs_of(*reg.set_of(a)) != 2 || g_built != 4) return 12;
     // many callers on a and b while other threads create/destroy more handles of K1 and finally
     // destroy a mid-flight
     std::atomic<bool> stop{false};
@@ -140,7 +147,7 @@ static int sharing_and_lifecycle() {
             std::mt19937_64 rng(77 + t);
             std::vector<uint8_t> buf;
             while (!stop) {
-                Handle<FakeDev>* h = (t & 1) ? a : b;
+                void* h = (t & 1) ? a : b;
                 Reg::Use u(reg, h);
                 if (!u.ok()) {
                     refused++;
@@ -165,7 +172,7 @@ static int sharing_and_lifecycle() {
     for (int t = 0; t < 4; t++)
         th.emplace_back([&] {
             for (int k = 0; k < 30; k++) {
-                Handle<FakeDev>* h;
+                void* h;
                 if (reg.create("K1", {0, 1, 2}, make, &h)) {
                     bad++;
                     return;
@@ -184,7 +191,7 @@ static int sharing_and_lifecycle() {
         Reg::Use u(reg, a);
         if (u.ok()) return 15;  // calls on a destroyed handle are refused
     }
-    if (reg.refs_of(*b->set) != 1 || g_alive != 4) return 16;
+    if (reg.refs_of(*reg.set_of(b)) != 1 || g_alive != 4) return 16;
     if (!reg.destroy(b)) return 17;  // the last K1 handle: its three devices go
     if (g_alive != 1 || reg.sets() != 1) return 18;
     if (!reg.destroy(c) || g_alive != 0 || reg.sets() != 0 || reg.handles() != 0) return 19;
@@ -196,9 +203,9 @@ static int sharing_and_lifecycle() {
 
 static int assignment() {
     Reg reg;
-    Handle<FakeDev>* h;
+    void* h;
     if (reg.create("K3", {0, 1, 2, 3}, make, &h)) return 30;
-    SharedSet<FakeDev>& s = *h->set;
+    SharedSet<FakeDev>& s = *reg.set_of(h);
     std::map<uint64_t, size_t> seen;
     std::vector<int> per(4, 0);
     for (uint64_t key = 0; key < 4000; key++) {
@@ -260,10 +267,121 @@ static int shutdown_in_flight() {
     return 0;
 }
 
+// A call's release racing destroy: the call's Use decrements its handle's count and,
+// through the test hook, lingers before unlocking; destroy issued in that window must wait for
+// it rather than free the handle under it.
+static std::atomic<int> g_hook_phase{0};
+static void linger_hook() {
+    if (g_hook_phase.load() != 1) return;
+    g_hook_phase = 2;  // decremented, handle lock still held
+    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    g_hook_phase = 3;
+}
+
+static int release_vs_destroy() {
+    Reg reg;
+    void* h;
+    if (reg.create("K4", {0}, make, &h)) return 50;
+    Reg::after_release_hook = linger_hook;
+    g_hook_phase = 0;
+    std::thread caller([&] {
+        Reg::Use u(reg, h);
+        if (!u.ok()) return;
+        g_hook_phase = 1;
+    });
+    while (g_hook_phase.load() < 2) std::this_thread::yield();
+    const bool destroyed = reg.destroy(h);
+    const int phase_at_return = g_hook_phase.load();
+    caller.join();
+    Reg::after_release_hook = nullptr;
+    if (!destroyed) return 51;
+    if (phase_at_return != 3) return 52;  // destroy returned while the call still held the handle
+    if (reg.destroy(h)) return 53;        // the token stays dead
+    // tokens are never reused: a new handle never takes a destroyed one's value
+    void* h2;
+    if (reg.create("K4", {0}, make, &h2)) return 54;
+    if (h2 == h || reg.set_of(h) != nullptr) return 55;
+    {
+        Reg::Use u(reg, h);
+        if (u.ok()) return 56;
+    }
+    if (!reg.destroy(h2) || reg.handles() != 0 || reg.sets() != 0) return 57;
+    return 0;
+}
+
+// sdfs_cdc_get_chunks_batch's split (Registry::run_shares) at 2 and 8 devices: every buffer is
+// processed exactly once, shares are contiguous and balanced, each share runs on its own device
+// and thread, and keyed routing (the write stream -> device map) is a stable function of the key.
+static int shares_and_routing() {
+    for (int n : {2, 8}) {
+        Reg reg;
+        std::vector<int> ords;
+        for (int i = 0; i < n; i++) ords.push_back(i);
+        void* h;
+        if (reg.create("K5/" + std::to_string(n), ords, make, &h)) return 60;
+        SharedSet<FakeDev>& s = *reg.set_of(h);
+        for (uint32_t nbuf : {0u, 1u, 63u, 64u, 127u, 128u, 129u, 1000u, 4096u, 16385u}) {
+            std::vector<std::atomic<int>> seen(nbuf);
+            for (auto& x : seen) x = 0;
+            std::vector<std::atomic<int>> per_dev(n);
+            for (auto& x : per_dev) x = 0;
+            std::mutex tm;
+            std::map<std::thread::id, int> threads;
+            size_t failed = 99;
+            const int rc = Reg::run_shares(
+                s, nbuf, 64,
+                [&](size_t d, uint32_t b0, uint32_t b1) {
+                    {
+                        std::lock_guard<std::mutex> lk(tm);
+                        threads[std::this_thread::get_id()]++;
+                    }
+                    if (s.load[d].load() < 1) return 1;  // the share is counted against its device
+                    per_dev[d] += (int)(b1 - b0);
+                    for (uint32_t b = b0; b < b1; b++) seen[b]++;
+                    return 0;
+                },
+                &failed);
+            if (rc) return 61;
+            for (uint32_t b = 0; b < nbuf; b++)
+                if (seen[b] != 1) return 62;
+            const uint32_t k = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, nbuf / 64));
+            int used = 0;
+            for (int d = 0; d < n; d++)
+                if (per_dev[d] > 0) used++;
+            if (nbuf && used != (int)k) return 63;
+            if (k > 1) {
+                if (threads.size() != k) return 64;  // one thread per share
+                for (uint32_t d = 0; d < k; d++)
+                    if (per_dev[d] != (int)(share_begin(nbuf, k, d + 1) - share_begin(nbuf, k, d))) return 65;
+            }
+            for (int d = 0; d < n; d++)
+                if (s.load[d].load() != 0) return 66;  // loads released
+        }
+        // a failing share is reported with its device
+        size_t failed = 99;
+        const int rc = Reg::run_shares(
+            s, 64u * n, 64, [&](size_t d, uint32_t, uint32_t) { return d == (size_t)n - 1 ? -3 : 0; }, &failed);
+        if (rc != -3 || failed != (size_t)n - 1) return 67;
+        // keyed routing: stable per key, spread over the set
+        std::vector<int> per(n, 0);
+        for (uint64_t key = 0; key < 8000; key++) {
+            const size_t i = Reg::pick(s, true, key);
+            if (i != (size_t)(share_mix64(key) % n) || Reg::pick(s, true, key) != i) return 68;
+            per[i]++;
+        }
+        for (int c : per)
+            if (c < 8000 / n * 8 / 10 || c > 8000 / n * 12 / 10) return 69;
+        if (!reg.destroy(h)) return 70;
+    }
+    return 0;
+}
+
 int main() {
     int rc = assignment();
     if (!rc) rc = shutdown_in_flight();
     if (!rc) rc = sharing_and_lifecycle();
+    if (!rc) rc = release_vs_destroy();
+    if (!rc) rc = shares_and_routing();
     printf(rc ? "FAIL %d\n" : "OK\n", rc);
     return rc;
 }
