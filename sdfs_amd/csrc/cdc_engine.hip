@@ -252,6 +252,9 @@ struct DevEngine {
     // queue behind a full-chip scan of the other stream; the fingerprint kernels still overlap.
     bool front_serial = false;
     bool front_recorded = false;
+    // Measurement probe (tuning: SDFS_FUSED_PROBE): the batch's fingerprint kernel is replaced by
+    // the fused scan + fingerprint kernel over the batch's own scan (again) and its tasks.
+    bool fused_probe = false;
     hipEvent_t ev_front = nullptr;
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
@@ -598,6 +601,10 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
         if (e->hash_split && e->prm.hash_algo != SDFS_CDC_MD5 && e->hash_variant == 0 &&
             max_tasks <= (uint64_t)e->num_cus * 128)
             HIP_TRY(launch_hash_split(ha, max_tasks, s));
+#ifdef SDFS_TUNING
+        else if (e->fused_probe && fused && nbuf >= (uint32_t)e->num_cus * 4)
+            HIP_TRY(launch_fused_probe(sa, ha, w->small.p + 2 * kMaxBins + 4, (int)e->prm.window, pk, e->num_cus, s));
+#endif
         else
             HIP_TRY(launch_hash(ha, max_tasks, e->hash_variant, s));
         t_end(e, t, s);
@@ -1168,6 +1175,7 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
             return fail(SDFS_CDC_EHIP, "scan-priority stream creation failed");
     }
     if (const char* v = getenv("SDFS_FRONT_SERIAL")) e->front_serial = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_FUSED_PROBE")) e->fused_probe = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif
