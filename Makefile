@@ -14,7 +14,11 @@ OBJS := $(SRCS:%=build/%.o)
 TUNING_OBJS := $(SRCS:%=build/tuning/%.o) build/tuning/cdc_sweep.o build/tuning/cdc_sweep_r3.o
 HDRS := $(CSRC)/cdc_internal.h $(CSRC)/cdc_device.h $(CSRC)/host_queue.h $(CSRC)/engine_share.h $(CSRC)/stream_order.h $(wildcard include/*.h)
 
-all: $(LIB) tuning tools oracle
+all: $(LIB) tuning tools oracle buildinfo
+
+# the commit the built libraries come from (bench.py reports it; the GPU box has no .git)
+buildinfo:
+	@git rev-parse --short=12 HEAD > sdfs_amd/BUILD_COMMIT 2>/dev/null && (git diff --quiet HEAD -- sdfs_amd include 2>/dev/null || sed -i 's/$$/+dirty/' sdfs_amd/BUILD_COMMIT) || true
 
 tuning: $(TUNING_LIB)
 
@@ -52,4 +56,4 @@ clean:
 	rm -rf build $(LIB) $(TUNING_LIB) tools/*.so jni/*.so tests/jni/*.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean tuning tools
+.PHONY: all oracle clean tuning tools buildinfo

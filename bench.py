@@ -112,10 +112,17 @@ def cpu_quota():
 
 
 def git_head() -> str:
+    """HEAD of the tree, or (on the GPU box, which gets no .git) the commit `make` recorded."""
     try:
-        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
-                              text=True, timeout=10).stdout.strip() or "unknown"
+        h = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                           text=True, timeout=10).stdout.strip()
+        if h:
+            return h
     except Exception:
+        pass
+    try:
+        return "built from " + open(os.path.join(ROOT, "sdfs_amd", "BUILD_COMMIT")).read().strip()
+    except OSError:
         return "unknown"
 
 

@@ -1239,7 +1239,8 @@ __global__ __launch_bounds__(256) void chunk_hash_persistent_kernel(HashArgs a) 
 //     share every SIMD until one queue runs dry.  ctr[0] / ctr[1]: zeroed item counters.
 //     Uniform batches whose buffers are exactly 64 segments (the fused cut walk) only.
 // ------------------------------------------------------------------------------------------
-template <int W, int PK, class CFG, int ALGO>
+// NS: scan-first waves per SIMD (0: the k-th waves of each SIMD with k even, i.e. two of four)
+template <int W, int PK, class CFG, int ALGO, int NS = 0>
 __global__ __launch_bounds__(1024, 1) void cdc_fused_kernel(ScanArgs a, HashArgs ha, uint32_t* ctr) {
     static_assert(CFG::kFuse == 2 && CFG::kChains == 1, "fused form: one chain, register-summary cut walk");
     constexpr int C = CFG::kCopies;
@@ -1259,7 +1260,7 @@ __global__ __launch_bounds__(1024, 1) void cdc_fused_kernel(ScanArgs a, HashArgs
     const uint64_t total = a.total_segs;
     const uint32_t nscan = a.fuse_resolve ? (uint32_t)(total >> 6) : 0u;
     const uint32_t htotal = ha.total ? *ha.total : 0u;
-    const bool scan_first = ((threadIdx.x >> 8) & 1) == 0;
+    const bool scan_first = NS == 0 ? ((threadIdx.x >> 8) & 1) == 0 : (int)(threadIdx.x >> 8) < NS;
     bool scan_left = nscan != 0, hash_left = htotal != 0;
     while (scan_left || hash_left) {
         const bool do_scan = scan_left && (scan_first || !hash_left);

@@ -254,7 +254,7 @@ struct DevEngine {
     bool front_recorded = false;
     // Measurement probe (tuning: SDFS_FUSED_PROBE): the batch's fingerprint kernel is replaced by
     // the fused scan + fingerprint kernel over the batch's own scan (again) and its tasks.
-    bool fused_probe = false;
+    int fused_probe = 0;  // form (cdc_sweep_r3.hip launch_fused_probe)
     hipEvent_t ev_front = nullptr;
     ScanVariantInfo scan_info{};
     uint32_t first_off = 0;
@@ -603,7 +603,8 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
             HIP_TRY(launch_hash_split(ha, max_tasks, s));
 #ifdef SDFS_TUNING
         else if (e->fused_probe && fused && nbuf >= (uint32_t)e->num_cus * 4)
-            HIP_TRY(launch_fused_probe(sa, ha, w->small.p + 2 * kMaxBins + 4, (int)e->prm.window, pk, e->num_cus, s));
+            HIP_TRY(launch_fused_probe(sa, ha, w->small.p + 2 * kMaxBins + 4, (int)e->prm.window, pk, e->num_cus,
+                                       e->fused_probe, s));
 #endif
         else
             HIP_TRY(launch_hash(ha, max_tasks, e->hash_variant, s));
@@ -1175,7 +1176,7 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
             return fail(SDFS_CDC_EHIP, "scan-priority stream creation failed");
     }
     if (const char* v = getenv("SDFS_FRONT_SERIAL")) e->front_serial = atoi(v) != 0;
-    if (const char* v = getenv("SDFS_FUSED_PROBE")) e->fused_probe = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_FUSED_PROBE")) e->fused_probe = atoi(v);
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif

@@ -188,7 +188,7 @@ hipError_t launch_scan_sweep_r3(const ScanArgs& a, int window, int pk, int varia
 // measurement probe (tuning build, SDFS_FUSED_PROBE): the fused scan + fingerprint kernel over the
 // batch's own scan (again: same slots, same values) and its fingerprint tasks
 hipError_t launch_fused_probe(const ScanArgs& a, const HashArgs& ha, uint32_t* ctr, int window, int pk, int grid,
-                              hipStream_t s);
+                              int form, hipStream_t s);
 hipError_t launch_scan_sweep(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
                              hipStream_t stream);
 hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);

@@ -84,14 +84,27 @@ hipError_t launch_scan_sweep_r3(const ScanArgs& a, int window, int pk, int varia
     }
 }
 
-hipError_t launch_fused_probe(const ScanArgs& a, const HashArgs& ha, uint32_t* ctr, int window, int pk, int grid,
-                              hipStream_t s) {
+template <int NS>
+static void fused_launch(const ScanArgs& a, const HashArgs& ha, uint32_t* ctr, int grid, hipStream_t s) {
     using Prod = ScanV51;  // the production scan form
-    if (window != 48 || pk != 2 || !a.uniform_len || !a.fuse_resolve) return hipErrorInvalidValue;
     if (ha.algo == 2)
-        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 2>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
+        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 2, NS>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
     else
-        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 0>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
+        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 0, NS>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
+}
+
+// form 1: two scan-first waves per SIMD (interleaved); 2 / 3 / 4: one / two / three scan-first
+// waves per SIMD (the first k waves of each SIMD)
+hipError_t launch_fused_probe(const ScanArgs& a, const HashArgs& ha, uint32_t* ctr, int window, int pk, int grid,
+                              int form, hipStream_t s) {
+    if (window != 48 || pk != 2 || !a.uniform_len || !a.fuse_resolve) return hipErrorInvalidValue;
+    switch (form) {
+    case 1: fused_launch<0>(a, ha, ctr, grid, s); break;
+    case 2: fused_launch<1>(a, ha, ctr, grid, s); break;
+    case 3: fused_launch<2>(a, ha, ctr, grid, s); break;
+    case 4: fused_launch<3>(a, ha, ctr, grid, s); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
