@@ -38,7 +38,7 @@ constexpr uint32_t kLimit64K = 65536 + kMfLimit - 1;  // below: 16-bit position 
 constexpr uint32_t kMaxDistance = 65535;
 constexpr uint32_t kScrBuckets = 1024;  // same-entry detection among one round's 64 probes
 constexpr int kLz4WgPerCu = 9;          // 17 KiB of LDS per one-wave workgroup: 9 fit in 160 KiB
-                                        // (latency-bound: throughput ~ waves in flight, scripts/lz4_grid_sweep.sh)
+                                        // (latency-bound: throughput ~ waves in flight, scripts/probes/lz4_grid_sweep.sh)
 
 struct Lz4Args {
     const uint8_t* data;
@@ -1165,7 +1165,7 @@ int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
 int launch_compress_impl(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
     // Auto: a batch with enough chunks to fill the chip one lane per chunk runs the hybrid (lanes
     // for compressible chunks, the wave kernel for the ones a lane bails on); smaller batches the
-    // wave kernel (scripts/lz4_batch_sweep.sh: the hybrid pays from ~50 000 chunks per 256 CUs).
+    // wave kernel (scripts/probes/lz4_batch_sweep.sh: the hybrid pays from ~50 000 chunks per 256 CUs).
     // n_max bounds a device-count batch, so the choice follows the capacity the caller gives.
     const int lane_mode = z->lane_mode >= 0 ? z->lane_mode
                                             : (a.n_max >= (uint64_t)z->num_cus * kHybridChunksPerCu ? 2 : 0);
