@@ -65,10 +65,21 @@ static int range_ok(jarray a, jsize start, jsize n) {
     return 1;
 }
 
+static __thread int t_fail_region;  /* next GetByteArrayRegion raises (stub_fail_next_region) */
+
 static void stub_GetByteArrayRegion(JNIEnv* env, jbyteArray a, jsize start, jsize n, jbyte* buf) {
     (void)env;
+    if (t_fail_region) {  /* as a JVM does for a bad region: nothing copied, exception pending */
+        t_fail_region = 0;
+        snprintf(t_exc_class, sizeof t_exc_class, "java/lang/ArrayIndexOutOfBoundsException");
+        snprintf(t_exc_msg, sizeof t_exc_msg, "stub: injected");
+        t_pending = 1;
+        return;
+    }
     if (a->kind == 1 && range_ok(a, start, n)) memcpy(buf, a->data + start, (size_t)n);
 }
+
+void stub_fail_next_region(void) { t_fail_region = 1; }
 
 static void stub_SetByteArrayRegion(JNIEnv* env, jbyteArray a, jsize start, jsize n, const jbyte* buf) {
     (void)env;

@@ -142,3 +142,44 @@ def test_jni_get_chunks_and_get_hash_vs_oracle(algo):
     st, ln, dg = j.new(2, 66), j.new(2, 66), j.new(1, 66 * dl)
     assert j.call("nativeGetChunks", h2, arr, 7, st, ln, dg) == len(O.chunk(data, prm)[0])
     j.call("nativeDestroy", h2)
+
+
+@pytest.mark.gpu
+def test_fill_failure_is_einval_with_its_own_message():
+    """A fill callback that fails (the JNI glue's GetByteArrayRegion raising) fails that call only:
+    SDFS_CDC_EINVAL with "fill callback failed" in sdfs_cdc_last_error (not an earlier, unrelated
+    message), count 0, the Java exception left pending; the engine keeps serving calls."""
+    from sdfs_amd import _lib
+    from sdfs_amd.engine import HipVariableSha256HashEngine
+    lib = _lib.load()
+    eng = HipVariableSha256HashEngine(device=0)
+    data = O.synth(O.SYNTH_SEED, 4242, 0, 262144).tobytes()
+    es, el, ed = O.chunk(data)
+    cap = eng.slot_cap(len(data))
+    st, ln = np.zeros(cap, np.uint32), np.zeros(cap, np.uint32)
+    dg = np.zeros((cap, 32), np.uint8)
+    n = ctypes.c_uint32(99)
+    cb = _lib.FILL_FN(lambda ctx, dst, ln_: -7)
+    rc = lib.sdfs_cdc_get_chunks_fill(eng._h, _lib.NO_STREAM, len(data), cb, None, st.ctypes.data, ln.ctypes.data,
+                                      dg.ctypes.data, cap, ctypes.byref(n))
+    assert rc == _lib.EINVAL and n.value == 0
+    assert "fill callback failed (-7)" in lib.sdfs_cdc_last_error().decode()
+    s2, l2, d2 = eng.chunk_arrays(data, fill=True)  # the engine still serves calls
+    assert s2.tolist() == es.tolist() and l2.tolist() == el.tolist() and (d2 == ed).all()
+    eng.destroy()
+    # through the glue: the injected ArrayIndexOutOfBoundsException stays the pending exception
+    j = Jni()
+    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, 0, 0)
+    assert h and j.exception() is None
+    arr = j.byte_array(data)
+    c = j.call("nativeSlotCap", h, len(data))
+    st, ln, dg = j.new(2, c), j.new(2, c), j.new(1, c * 32)
+    j.stub.stub_fail_next_region()
+    assert j.call("nativeGetChunks", h, arr, -1, st, ln, dg) == -1
+    cls, _ = j.exception()
+    assert cls == "java/lang/ArrayIndexOutOfBoundsException"
+    assert "fill callback failed" in lib.sdfs_cdc_last_error().decode()
+    assert j.call("nativeGetChunks", h, arr, -1, st, ln, dg) == len(es) and j.exception() is None
+    for a in (arr, st, ln, dg):
+        j.stub.stub_free(a)
+    j.call("nativeDestroy", h)
