@@ -151,6 +151,21 @@ def main():
     }
     if CONFIG == "dedup":
         res["duplicate_buffers"] = dup_bufs
+    # per-kernel breakdown of the getChunks pipeline (HIP events around every kernel, untimed above)
+    # and the chunk-length tail, which sets the fingerprint kernel's floor (one serial SHA-256
+    # chain per chunk)
+    eng.set_timing(STEPS)
+    for _ in range(STEPS):
+        batch.run(buffer_id_base=0, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    res["kernels_ms"] = {k: round(v, 4) for k, v in eng.kernel_times().items() if v}
+    eng.set_timing(0)
+    lens = batch.lens.view(batch.nbuf, batch.cap)
+    valid = torch.arange(batch.cap, device=lens.device)[None, :] < batch.counts[:, None]
+    cl = lens[valid].to(torch.int64)
+    top = torch.topk(cl, min(8, cl.numel())).values.tolist()
+    res["chunk_len"] = {"max": int(cl.max().item()), "top8": top,
+                        "over_64KiB": int((cl > 65536).sum().item()), "over_32KiB": int((cl > 32768).sum().item())}
     # two batches in flight on two streams (two engines): batch i+1's scan overlaps the tail of
     # batch i's fingerprinting, where the longest chunks' serial SHA-256 leaves the GPU half idle
     eng2 = HipVariableSha256HashEngine(config=cfg)

@@ -1239,8 +1239,10 @@ __global__ __launch_bounds__(256) void chunk_hash_persistent_kernel(HashArgs a) 
 //     share every SIMD until one queue runs dry.  ctr[0] / ctr[1]: zeroed item counters.
 //     Uniform batches whose buffers are exactly 64 segments (the fused cut walk) only.
 // ------------------------------------------------------------------------------------------
-// NS: scan-first waves per SIMD (0: the k-th waves of each SIMD with k even, i.e. two of four)
-template <int W, int PK, class CFG, int ALGO, int NS = 0>
+// NS: scan-first waves per SIMD (0: the k-th waves of each SIMD with k even, i.e. two of four).
+// SP > 0: scan items run at issue priority SP and fingerprint items at 0 (the scan's latency-bound
+// chain issues first, the fingerprint's independent VALU work fills the rest)
+template <int W, int PK, class CFG, int ALGO, int NS = 0, int SP = 0>
 __global__ __launch_bounds__(1024, 1) void cdc_fused_kernel(ScanArgs a, HashArgs ha, uint32_t* ctr) {
     static_assert(CFG::kFuse == 2 && CFG::kChains == 1, "fused form: one chain, register-summary cut walk");
     constexpr int C = CFG::kCopies;
@@ -1272,11 +1274,17 @@ __global__ __launch_bounds__(1024, 1) void cdc_fused_kernel(ScanArgs a, HashArgs
                 scan_left = false;
                 continue;
             }
+            if constexpr (SP > 0) __builtin_amdgcn_s_setprio(SP);
             scan_iter<W, PK, CFG>(a, tab, lhist, (uint64_t)it * 64, lane, 64, total, lane, c8, push_base, pa_reg, qa_reg);
+            if constexpr (SP > 0) __builtin_amdgcn_s_setprio(0);
         } else {
             const uint32_t i0 = it * 64;
             if (i0 >= htotal) {
                 hash_left = false;
+                continue;
+            }
+            if constexpr (SP > 0) {
+                if (i0 + lane < htotal) hash_task<ALGO, 16, true>(ha, i0 + lane);
                 continue;
             }
             // issue priority for waves of long chunks, as in chunk_hash_kernel (task i0 is the
@@ -1317,14 +1325,16 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
+// One 64-chunk group of the latency form: tasks base .. base + 63 (those below ntask).  Wave 0 of
+// the workgroup produces, wave 1 consumes; any further waves (the long-chunk groups of the
+// throughput kernel below run in its 256-thread workgroups) only take part in the barriers.
 template <int ALGO>
-__global__ __launch_bounds__(128) void chunk_hash_split_kernel(HashArgs a) {
+__device__ __forceinline__ void hash_split_group(const HashArgs& a, uint32_t base, uint32_t ntask, uint32_t wave,
+                                                 uint4 (&wk)[2][16][kSplitTasks]) {
     static_assert(ALGO != 2, "MD5 has no split form");
-    __shared__ uint4 wk[2][16][kSplitTasks];  // [buffer][t / 4][lane] = W[t..t+3] + K[t..t+3]
     const uint32_t lane = threadIdx.x & 63;
-    const bool producer = threadIdx.x < 64;
-    const uint32_t i = blockIdx.x * kSplitTasks + lane;
-    const uint32_t ntask = *a.total;
+    const bool producer = wave == 0, consumer = wave == 1;
+    const uint32_t i = base + lane;
     uint32_t slot = 0, b = 0, k = 0, cs = 0, len = 0, nfull = 0, nblocks = 0;
     const uint8_t* p = a.zero_page;
     if (i < ntask) {
@@ -1338,8 +1348,7 @@ __global__ __launch_bounds__(128) void chunk_hash_split_kernel(HashArgs a) {
         nfull = len >> 6;
         nblocks = (len + 8) / 64 + 1;
     }
-    const uint32_t maxnb = wave_max_u32(nblocks);  // identical in both waves (same 64 tasks)
-    if (blockIdx.x * kSplitTasks >= ntask) return;  // whole workgroup past the end (uniform)
+    const uint32_t maxnb = wave_max_u32(nblocks);  // identical in every wave (same 64 tasks)
     uint32_t s[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
     uint4 nx[4];
     if (producer) load_block64(nx, nfull ? p : a.zero_page);
@@ -1393,7 +1402,7 @@ __global__ __launch_bounds__(128) void chunk_hash_split_kernel(HashArgs a) {
                     }
                 }
             }
-        } else if (it >= 1) {
+        } else if (consumer && it >= 1) {
             const uint32_t blk = it - 1;
             if (blk < nblocks) {
                 const uint4(*src)[kSplitTasks] = wk[blk & 1];
@@ -1417,7 +1426,42 @@ __global__ __launch_bounds__(128) void chunk_hash_split_kernel(HashArgs a) {
         }
         __syncthreads();
     }
-    if (!producer && i < ntask) store_digest<ALGO>(a, slot, b, k, cs, len, s);
+    if (consumer && i < ntask) store_digest<ALGO>(a, slot, b, k, cs, len, s);
+}
+
+template <int ALGO>
+__global__ __launch_bounds__(128) void chunk_hash_split_kernel(HashArgs a) {
+    __shared__ uint4 wk[2][16][kSplitTasks];  // [buffer][t / 4][lane] = W[t..t+3] + K[t..t+3]
+    const uint32_t ntask = *a.total;
+    if (blockIdx.x * kSplitTasks >= ntask) return;  // whole workgroup past the end (uniform)
+    hash_split_group<ALGO>(a, blockIdx.x * kSplitTasks, ntask, threadIdx.x >> 6, wk);
+}
+
+// ------------------------------------------------------------------------------------------
+// 5c. throughput form with the longest chunks in the latency form (backup profile: maxLen
+//     128 KiB).  A chunk's SHA-256 is one serial chain, so a batch's longest chunk sets a floor
+//     under chunk_hash_kernel (a 55 KB chunk: 869 blocks x ~2.8 us with the GPU otherwise idle at
+//     the end, 3.50 vs 3.03 ms per 4 GiB with every chunk clipped to 32 KiB,
+//     scripts/backup_tail_probe.py).  Tasks 0 .. *nlong-1 (the chunks of more than kLongBlocks
+//     blocks, at the head of the longest-first list) go to the first workgroups in 64-chunk
+//     producer/consumer groups (section 5b: ~905 instead of ~1 423 instructions per block on the
+//     chain); the rest run one lane per chunk as in chunk_hash_kernel.
+// ------------------------------------------------------------------------------------------
+template <int ALGO>
+__global__ __launch_bounds__(256) void chunk_hash_long_kernel(HashArgs a) {
+    __shared__ uint4 wk[2][16][kSplitTasks];
+    uint32_t nl = __builtin_amdgcn_readfirstlane(*a.nlong);
+    if (nl > kLongSplitMax) nl = 0;
+    const uint32_t lg = (nl + kSplitTasks - 1) / kSplitTasks;  // long-chunk workgroups
+    if (blockIdx.x < lg) {
+        hash_split_group<ALGO>(a, blockIdx.x * kSplitTasks, nl, threadIdx.x >> 6, wk);
+        return;
+    }
+    const uint32_t i = nl + (blockIdx.x - lg) * 256 + threadIdx.x;
+    if (i >= *a.total) return;
+    const uint32_t nb = __builtin_amdgcn_readfirstlane(sha_blocks(a.clens[a.tasks[i]]));
+    if (nb > 256) __builtin_amdgcn_s_setprio(1);
+    hash_task<ALGO, 16, true>(a, i);
 }
 
 }  // namespace sdfs

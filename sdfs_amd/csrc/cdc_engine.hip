@@ -171,12 +171,13 @@ struct Workspace {
     DevBuf<uint32_t> rec_base;
     DevBuf<uint32_t> tasks;
     DevBuf<uint32_t> spec_starts, spec_cnt, spec_next;  // sectioned cut walk of very long buffers
+    DevBuf<uint32_t> join;  // its parallel stitch: kJoinWords per section, then one flag per buffer
     DevBuf<uint32_t> x_scratch;  // extent ordering (getHash in bulk): hist | cursor | total, starts | tasks
     hipEvent_t free_ev = nullptr;
     bool pending = false;  // free_ev recorded and possibly not reached yet
     uint32_t* overflow() const { return small.p + 2 * kMaxBins; }
     void release_all() {
-        for (auto* b : {&bitmap, &small, &rec_base, &tasks, &spec_starts, &spec_cnt, &spec_next, &x_scratch})
+        for (auto* b : {&bitmap, &small, &rec_base, &tasks, &spec_starts, &spec_cnt, &spec_next, &join, &x_scratch})
             b->release();
         seg_prefix.release();
     }
@@ -244,6 +245,9 @@ struct DevEngine {
     uint32_t scan_max_block = kScanThreads;  // widest scan workgroup (tuning build: SDFS_SCAN_MAX_BLOCK)
     bool hash_split = true;                  // latency form of the fingerprint for small batches (tuning: SDFS_HASH_SPLIT)
     bool small_seg = true;                   // short scan segments for small batches (tuning: SDFS_SMALL_SEG)
+    bool long_split = true;                  // latency form for chunks > 32 KiB (tuning: SDFS_LONG_SPLIT)
+    bool par_stitch = true;                  // parallel join/place of long buffers' sections (tuning: SDFS_PAR_STITCH)
+    uint32_t sec_log2 = 20;                  // section length of long buffers' cut walk (tuning: SDFS_SEC_LOG2)
     bool scan_prio = false;                  // pre-fingerprint stages on a high-priority stream (tuning: SDFS_SCAN_PRIO)
     hipStream_t s_scan = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -338,7 +342,8 @@ int ws_acquire(DevEngine* e, const WsNeed& nd, hipStream_t s, Workspace** out, W
                       w->rec_base.fits(nd.rec_base) && w->tasks.fits(nd.tasks) &&
                       (!nd.seg_prefix || w->seg_prefix.fits(nd.seg_prefix)) &&
                       (!nd.spec_items || (w->spec_starts.fits(nd.spec_starts) && w->spec_cnt.fits(nd.spec_items) &&
-                                          w->spec_next.fits(nd.spec_items))) &&
+                                          w->spec_next.fits(nd.spec_items) &&
+                                          w->join.fits(nd.spec_items * kJoinWords + nd.rec_base))) &&
                       (!nd.x_scratch || w->x_scratch.fits(nd.x_scratch));
     if (!fits && w->pending) HIP_TRY(hipEventSynchronize(w->free_ev));  // never free memory in use
     HIP_TRY(w->bitmap.ensure(std::max<uint64_t>(nd.bitmap_words, 2)));
@@ -350,6 +355,7 @@ int ws_acquire(DevEngine* e, const WsNeed& nd, hipStream_t s, Workspace** out, W
         HIP_TRY(w->spec_starts.ensure(nd.spec_starts));
         HIP_TRY(w->spec_cnt.ensure(nd.spec_items));
         HIP_TRY(w->spec_next.ensure(nd.spec_items));
+        HIP_TRY(w->join.ensure(nd.spec_items * kJoinWords + nd.rec_base));  // + one flag per buffer
     }
     if (nd.x_scratch) HIP_TRY(w->x_scratch.ensure(nd.x_scratch));
     if (w->pending) HIP_TRY(hipStreamWaitEvent(s, w->free_ev, 0));
@@ -385,7 +391,7 @@ WsNeed pipeline_need(const DevEngine* e, uint64_t data_bytes, uint32_t nbuf, uin
     nd.tasks = (uint64_t)nbuf * cap;
     if (!uniform_len) nd.seg_prefix = (uint64_t)nbuf + 1;
     const uint64_t mbl = uniform_len ? uniform_len : max_buf_len;
-    const uint32_t sec = resolve_section_len(mbl, e->prm.max_len);
+    const uint32_t sec = resolve_section_len(mbl, e->prm.max_len, e->sec_log2);
     *sec_len_out = sec;
     *nsec_out = *spec_cap_out = 0;
     if (sec) {
@@ -510,6 +516,10 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
         ra.spec_starts = w->spec_starts.p;
         ra.spec_cnt = w->spec_cnt.p;
         ra.spec_next = w->spec_next.p;
+        if (e->par_stitch) {
+            ra.join = w->join.p;
+            ra.join_bad = w->join.p + (uint64_t)nbuf * nsec * kJoinWords;
+        }
     }
     // one wave = one buffer: the scan kernel resolves the cuts in its epilogue
     const bool fused = e->scan_info.fuse && uniform_len && (e->scan_info.chains == 1 || e->scan_info.fuse == 2) &&
@@ -593,6 +603,19 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     ha.algo = e->prm.hash_algo;
     ha.wave_ctr = w->small.p + 2 * kMaxBins + 2;  // zeroed with the rest of `small` above
     ha.persist_grid = (uint32_t)(e->num_cus * e->hash_wg_per_cu);
+    {
+        // chunks of more than kLongBlocks SHA blocks (a maxLen above 32 KiB: the backup profile)
+        // head the longest-first list; after the scatter, cursor[b] = tasks in bins >= b, so
+        // cursor[tb + 1] counts the chunks of bins wholly above kLongBlocks
+        const uint32_t tb = kLongBlocks >> e->bin_shift;
+        const uint32_t maxblocks = (e->prm.max_len + 8) / 64 + 1;
+        if (e->long_split && e->prm.max_len > 32768 && ((tb + 1) << e->bin_shift) <= maxblocks && tb + 1 < e->nbins) {
+            ha.nlong = cursor + tb + 1;
+            const uint64_t mbl = uniform_len ? uniform_len : max_buf_len;
+            const uint64_t per = mbl / ((uint64_t)kLongBlocks * 64 - 72) + 1;
+            ha.max_long = (uint32_t)std::min<uint64_t>((uint64_t)nbuf * per, (uint64_t)nbuf * out->cap);
+        }
+    }
     {
         const int t = t_begin(e, K_HASH, s);
         const uint64_t max_tasks = (uint64_t)nbuf * out->cap;
@@ -929,11 +952,12 @@ struct QueueBackend {
         HIP_TRY(w.x_scratch.ensure(kExtentScratchWords + 2ull * max_reqs));
         // a request long enough for the sectioned cut walk travels in a slot of its own (admits),
         // so one buffer's sections bound its speculative-walk scratch (pipeline_need)
-        if (const uint32_t sec = resolve_section_len(max_req, e->prm.max_len)) {
+        if (const uint32_t sec = resolve_section_len(max_req, e->prm.max_len, e->sec_log2)) {
             const uint64_t nsec = (max_req + sec - 1) / sec;
             HIP_TRY(w.spec_starts.ensure(nsec * (sec / (e->first_off + 1) + 2)));
             HIP_TRY(w.spec_cnt.ensure(nsec));
             HIP_TRY(w.spec_next.ensure(nsec));
+            HIP_TRY(w.join.ensure(nsec * kJoinWords + 1));
         }
         HIP_TRY(hipEventCreateWithFlags(&d->kdone, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&d->ws.free_ev, hipEventDisableTiming));
@@ -949,7 +973,7 @@ struct QueueBackend {
     }
 
     // getChunks requests whose cut walk runs in sections (buffers of 4 MiB and more) travel alone
-    bool is_long(uint64_t len) const { return resolve_section_len(len, e->prm.max_len) != 0; }
+    bool is_long(uint64_t len) const { return resolve_section_len(len, e->prm.max_len, e->sec_log2) != 0; }
 
     bool admits(const QSlot& s, const QReq& r) {
         if (r.kind != QReq::kChunks) return true;
@@ -1166,6 +1190,9 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_HASH_SPLIT")) e->hash_split = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SMALL_SEG")) e->small_seg = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_LONG_SPLIT")) e->long_split = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_PAR_STITCH")) e->par_stitch = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SEC_LOG2")) e->sec_log2 = (uint32_t)std::max(16, std::min(atoi(v), 24));
     if (const char* v = getenv("SDFS_SCAN_PRIO")) e->scan_prio = atoi(v) != 0;
     if (e->scan_prio) {
         int lo = 0, hi = 0;

@@ -58,9 +58,16 @@ struct ResolveArgs {
     uint32_t* spec_starts; // [nbuf * nsec * spec_cap]
     uint32_t* spec_cnt;    // [nbuf * nsec]
     uint32_t* spec_next;   // [nbuf * nsec] first chunk start at or past the section end
+    // parallel stitch (cdc_resolve_join_kernel / cdc_resolve_place_kernel): per section
+    // {first speculative start on the true chain or kJoinUnmerged, extra true starts, ...},
+    // then one flag per buffer (1 = the sequential stitch walks it)
+    uint32_t* join;        // [nbuf * nsec * kJoinWords]
+    uint32_t* join_bad;    // [nbuf]
 };
+constexpr uint32_t kJoinExtra = 8;  // true chunk starts a section may take before its chains meet
+constexpr uint32_t kJoinWords = 2 + kJoinExtra;
 // Section length of the sectioned cut walk for a buffer of `len` bytes (0 = not sectioned).
-uint32_t resolve_section_len(uint64_t len, uint32_t max_len);
+uint32_t resolve_section_len(uint64_t len, uint32_t max_len, uint32_t sec_log2 = 20);
 
 struct ScanArgs {
     const uint8_t* data;
@@ -115,6 +122,13 @@ struct ScatterArgs {
     uint32_t* tasks;
 };
 
+// Long chunks (chunk_hash_long_kernel): more than kLongBlocks SHA-256 blocks, i.e. > 32 KiB - 8
+// bytes — only a maxLen above the default makes them.  More long chunks than kLongSplitMax fill
+// the chip on their own (their chains no longer form a tail) and the latency form's half-idle
+// workgroups would cost throughput, so then every chunk takes the lane form.
+constexpr uint32_t kLongBlocks = 512;
+constexpr uint32_t kLongSplitMax = 64 * 256;
+
 struct HashArgs {
     const uint8_t* data;
     const uint64_t* offs;
@@ -133,6 +147,11 @@ struct HashArgs {
     uint32_t persist_grid;     // workgroups of the persistent variant (0 = not used)
     uint32_t* wave_ctr;        // [1] zeroed task counter of the persistent variant
     const uint8_t* zero_page;  // 256 zero bytes: target of the branch-free next-block load past a chunk's last whole block
+    // long-chunk split (chunk_hash_long_kernel): [1] the number of tasks of more than kLongBlocks
+    // SHA blocks (they head the longest-first list), and a host bound on it for the grid; null /
+    // 0 = one lane per chunk throughout
+    const uint32_t* nlong;
+    uint32_t max_long;
 };
 
 // Longest-first order of arbitrary chunk extents (getHash in bulk): tasks[] = extent indices,

@@ -339,6 +339,153 @@ __global__ __launch_bounds__(256) void cdc_resolve_spec_kernel(ResolveArgs a) {
     }
 }
 
+// Parallel stitch, step 1 (join): one wave per (buffer, section j >= 1).  The true chain enters
+// section j at spec_next[j - 1], the first start the chain of section j - 1 reaches past its end
+// (that chain is the true one once section j - 1 has joined, by induction from section 0, whose
+// speculative walk starts where the buffer does).  From there the wave takes true steps until it
+// lands on one of section j's speculative starts — from that start on the two chains are one.
+// join[item] = {index of that start (cnt when the true chain only passes through, or
+// kJoinUnmerged: more than kJoinExtra steps, or it leaves the section elsewhere than
+// spec_next[j]), number of extra true starts, the extra starts}.  On random data the chains meet
+// within a chunk or two; a buffer with any unmerged section is left to the sequential stitch.
+constexpr uint32_t kJoinUnmerged = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(256) void cdc_resolve_join_kernel(ResolveArgs a) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nitems = a.nbuf * a.nsec;
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < nitems; item += nw) {
+        const uint32_t b = item / a.nsec, j = item - b * a.nsec;
+        const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
+        const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
+        const uint32_t r0 = j * a.sec_len;
+        uint32_t* jo = a.join + (uint64_t)item * kJoinWords;
+        uint32_t m = 0, nx = 0;
+        if (j > 0 && r0 < len) {
+            const uint32_t r1 = min(r0 + a.sec_len, len);
+            const uint32_t cm = a.spec_cnt[item];
+            const uint32_t* sp = a.spec_starts + (uint64_t)item * a.spec_cap;
+            const uint64_t word0 = off >> 5;
+            uint32_t p = a.spec_next[item - 1];
+            if (p >= len) {
+                m = cm;  // the chain ended before this section: none of its speculative starts is a cut
+            } else {
+                for (;;) {
+                    if (p >= r1) {  // passed through without meeting: fine if it leaves where they do
+                        m = p == a.spec_next[item] ? cm : kJoinUnmerged;
+                        break;
+                    }
+                    int32_t found = -1;
+                    for (uint32_t j0 = 0; j0 < cm; j0 += 64) {
+                        const uint32_t e = j0 + lane < cm ? sp[j0 + lane] : 0xFFFFFFFFu;
+                        const uint64_t hit = __ballot(e == p);
+                        if (hit) {
+                            found = (int32_t)(j0 + __builtin_ctzll(hit));
+                            break;
+                        }
+                        if (__ballot(e > p)) break;  // sorted: p is not a speculative start
+                    }
+                    if (found >= 0) {
+                        m = (uint32_t)found;
+                        break;
+                    }
+                    if (nx == kJoinExtra) {
+                        m = kJoinUnmerged;
+                        break;
+                    }
+                    const uint32_t lo = p + a.first_off;
+                    const uint32_t forced = p + a.max_len - 1;
+                    const uint32_t hi = forced < len - 1 ? forced : len - 1;
+                    int64_t k = -1;
+                    if (lo <= hi) k = find_first_wide(a.bitmap, word0, lo, hi, lane);
+                    if (k < 0) k = (int64_t)hi;
+                    if (lane == 0) jo[2 + nx] = p;
+                    nx++;
+                    p = (uint32_t)k + 1;
+                }
+            }
+        }
+        if (lane == 0) {
+            jo[0] = m;
+            jo[1] = nx;
+        }
+    }
+}
+
+// Parallel stitch, step 2 (place): one wave per (buffer, section) of a buffer whose sections all
+// joined: the section's chunks are its extra true starts, then its speculative starts from the
+// joining one on, each ending where the next begins (the last at spec_next: the section's chain is
+// the true one).  The slot offset is the sum of the earlier sections' chunk counts.
+__global__ __launch_bounds__(256) void cdc_resolve_place_kernel(ResolveArgs a) {
+    __shared__ uint32_t lhist[kMaxBins];
+    for (uint32_t i = threadIdx.x; i < a.nbins; i += 256) lhist[i] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nitems = a.nbuf * a.nsec;
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6); item < nitems; item += nw) {
+        const uint32_t b = item / a.nsec, j = item - b * a.nsec;
+        const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
+        const uint32_t nsb = (len + a.sec_len - 1) / a.sec_len;  // sections of this buffer
+        if (j >= nsb) continue;
+        const uint32_t* jb = a.join + (uint64_t)b * a.nsec * kJoinWords;
+        const uint32_t* cb = a.spec_cnt + (uint64_t)b * a.nsec;
+        // every section joined?  chunks before this section, and in the whole buffer
+        bool bad = false;
+        uint32_t before = 0, all = 0;
+        for (uint32_t s0 = 0; s0 < nsb; s0 += 64) {
+            const uint32_t sj = s0 + lane;
+            uint32_t n = 0;
+            if (sj < nsb) {
+                const uint32_t mj = jb[(uint64_t)sj * kJoinWords];
+                if (mj == kJoinUnmerged) bad = true;
+                else n = jb[(uint64_t)sj * kJoinWords + 1] + cb[sj] - mj;
+            }
+            if (__ballot(bad)) {
+                bad = true;
+                break;
+            }
+            uint32_t nb = sj < j ? n : 0;
+            for (int o = 32; o >= 1; o >>= 1) {
+                nb += __shfl_xor(nb, o);
+                n += __shfl_xor(n, o);
+            }
+            before += nb;
+            all += n;
+        }
+        if (bad) {
+            if (j == 0 && lane == 0) a.join_bad[b] = 1u;
+            continue;
+        }
+        if (j == 0 && lane == 0) {
+            a.join_bad[b] = 0u;
+            a.counts[b] = all < a.cap ? all : a.cap;
+            if (all > a.cap) atomicOr(a.overflow, 1u);
+        }
+        const uint32_t* jo = jb + (uint64_t)j * kJoinWords;
+        const uint32_t m = jo[0], nx = jo[1], cm = cb[j];
+        const uint32_t* sp = a.spec_starts + (uint64_t)item * a.spec_cap;
+        const uint32_t n = nx + cm - m;
+        const uint32_t nxt = a.spec_next[item];
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t st = i < nx ? jo[2 + i] : sp[m + i - nx];
+            const uint32_t en = i + 1 < nx ? jo[3 + i] : (i + 1 < n ? sp[m + i + 1 - nx] : nxt);
+            const uint32_t c = before + i;
+            if (c < a.cap) {
+                const uint64_t slot = (uint64_t)b * a.cap + c;
+                a.starts[slot] = st;
+                a.clens[slot] = en - st;
+                uint32_t bin = sha_blocks(en - st) >> a.bin_shift;
+                bin = bin < a.nbins ? bin : a.nbins - 1;
+                atomicAdd(&lhist[bin], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.nbins; i += 256)
+        if (lhist[i]) atomicAdd(&a.hist[i], lhist[i]);
+}
+
 // Stitch: one wave per buffer follows the true cut chain.  Where it lands on a section's
 // speculative chunk start the two chains coincide from there on (same greedy rule, same bits),
 // so the rest of that section's list is copied wave-parallel; otherwise it takes one true step
@@ -350,6 +497,7 @@ __global__ __launch_bounds__(256) void cdc_resolve_stitch_kernel(ResolveArgs a) 
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nw = gridDim.x * 4;
     for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < a.nbuf; b += nw) {
+        if (a.join_bad && !a.join_bad[b]) continue;  // placed by cdc_resolve_place_kernel
         const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
         const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
         const uint64_t word0 = off >> 5;
@@ -422,10 +570,14 @@ __global__ __launch_bounds__(256) void cdc_resolve_stitch_kernel(ResolveArgs a) 
         if (lhist[i]) atomicAdd(&a.hist[i], lhist[i]);
 }
 
-uint32_t resolve_section_len(uint64_t len, uint32_t max_len) {
-    // sections of 1 Mi positions for buffers of 4 MiB and more (40 MiB backup buffers: 40 sections)
-    if (len < (4ull << 20) || len >= (1ull << 31) || (uint64_t)max_len + 64 >= 32ull * kResStride) return 0;
-    return 1u << 20;
+uint32_t resolve_section_len(uint64_t len, uint32_t max_len, uint32_t sec_log2) {
+    // sections of 2^sec_log2 positions for buffers of 4 MiB and more (40 MiB backup buffers at the
+    // default 1 Mi: 40 sections); a section must hold a chunk of max_len
+    const uint64_t sec = 1ull << sec_log2;
+    if (len < (4ull << 20) || len >= (1ull << 31) || (uint64_t)max_len + 64 >= 32ull * kResStride ||
+        sec < 2ull * max_len)
+        return 0;
+    return (uint32_t)sec;
 }
 
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
@@ -433,8 +585,12 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
     if (a.sec_len && a.spec_starts && a.nbuf) {
         // very long buffers: speculative walk per section (one workgroup each), then stitch
         const uint64_t items = (uint64_t)a.nbuf * a.nsec;
-        hipLaunchKernelGGL(cdc_resolve_spec_kernel, dim3((uint32_t)std::min<uint64_t>((items + 3) / 4, 1u << 20)),
-                           dim3(256), 0, s, a);
+        const uint32_t g = (uint32_t)std::min<uint64_t>((items + 3) / 4, 1u << 20);
+        hipLaunchKernelGGL(cdc_resolve_spec_kernel, dim3(g), dim3(256), 0, s, a);
+        if (a.join && a.join_bad) {
+            hipLaunchKernelGGL(cdc_resolve_join_kernel, dim3(g), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(cdc_resolve_place_kernel, dim3(g), dim3(256), 0, s, a);
+        }
         hipLaunchKernelGGL(cdc_resolve_stitch_kernel, dim3((a.nbuf + 3) / 4), dim3(256), 0, s, a);
         return hipGetLastError();
     }
@@ -567,6 +723,16 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
 #else
         return hipErrorInvalidValue;
 #endif
+    }
+    if (a.nlong && a.algo != 2) {
+        // long chunks possible (maxLen above 32 KiB): they take the latency form (chunk_hash_long_kernel)
+        const uint32_t lg = (uint32_t)(((uint64_t)std::min<uint64_t>(a.max_long, kLongSplitMax) + kSplitTasks - 1) /
+                                       kSplitTasks);
+        if (a.algo == 0)
+            hipLaunchKernelGGL((chunk_hash_long_kernel<0>), dim3(blocks + lg), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((chunk_hash_long_kernel<1>), dim3(blocks + lg), dim3(256), 0, s, a);
+        return hipGetLastError();
     }
     // production: next-block prefetch issued unconditionally (ABL bit 16; interleaved A/B 2.762 ->
     // 2.744 ms median, profiles/r01/probes/hash_true_prefetch_ab.jsonl) and issue priority for

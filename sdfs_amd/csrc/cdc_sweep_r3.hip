@@ -84,13 +84,13 @@ hipError_t launch_scan_sweep_r3(const ScanArgs& a, int window, int pk, int varia
     }
 }
 
-template <int NS>
+template <int NS, int SP = 0>
 static void fused_launch(const ScanArgs& a, const HashArgs& ha, uint32_t* ctr, int grid, hipStream_t s) {
     using Prod = ScanV51;  // the production scan form
     if (ha.algo == 2)
-        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 2, NS>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
+        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 2, NS, SP>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
     else
-        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 0, NS>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
+        hipLaunchKernelGGL((cdc_fused_kernel<48, 2, Prod, 0, NS, SP>), dim3(grid), dim3(1024), 0, s, a, ha, ctr);
 }
 
 // form 1: two scan-first waves per SIMD (interleaved); 2 / 3 / 4: one / two / three scan-first
@@ -103,6 +103,9 @@ hipError_t launch_fused_probe(const ScanArgs& a, const HashArgs& ha, uint32_t* c
     case 2: fused_launch<1>(a, ha, ctr, grid, s); break;
     case 3: fused_launch<2>(a, ha, ctr, grid, s); break;
     case 4: fused_launch<3>(a, ha, ctr, grid, s); break;
+    case 5: fused_launch<1, 2>(a, ha, ctr, grid, s); break;  // 5-7: scan items at issue priority 2
+    case 6: fused_launch<0, 2>(a, ha, ctr, grid, s); break;
+    case 7: fused_launch<3, 2>(a, ha, ctr, grid, s); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -673,3 +673,55 @@ def test_scan_variants_agree():
     r = subprocess.run([sys.executable, "-c", _SCAN_VARIANT_CHECK], capture_output=True, text=True, env=env,
                        timeout=110, cwd=root)
     assert r.returncode == 0 and "scan variants ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+# ---------------------------------------------------------------- chunks longer than 32 KiB
+@pytest.mark.parametrize("algo", [O.SHA256, O.SHA256_160, O.MD5])
+@pytest.mark.parametrize("mask", [0xFFFFFF, 0xFFFF], ids=["forced", "mixed"])
+def test_device_long_chunks_latency_form(algo, mask):
+    """maxLen 128 KiB (the backup profile) makes chunks of more than 512 SHA-256 blocks; those head
+    the longest-first task list and take the two-wave latency form inside chunk_hash_long_kernel
+    (SHA-256 / SHA-256/160; MD5 keeps one lane per chunk).  A 24-bit predicate makes nearly every
+    chunk a forced 128 KiB cut (2 048 long chunks, 32 latency-form groups), a 16-bit one a mix of
+    4 KiB .. 128 KiB chunks; every chunk of every buffer against the oracle."""
+    prm = P(max_len=131072, pred_mask=mask, hash_algo=algo)
+    e = engine_for(prm)
+    nbuf, L = 64, 4 * 2**20
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=L, records=False)
+    batch.fill_streams(first_stream=910, bufs_per_stream=1)
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    nlong = int(sum((ln[b, :counts[b]] > 32768).sum() for b in range(nbuf)))
+    assert nlong > (1500 if mask == 0xFFFFFF else 64), nlong
+    _check_batch_against_oracle(batch, counts, st, ln, dg, prm, 1, 910, None)
+
+
+def test_device_long_chunks_beyond_split_cap():
+    """More long chunks than kLongSplitMax (16 384) in one batch: every chunk takes the lane form
+    (the latency form would cost throughput there).  520 x 4 MiB with forced 128 KiB cuts =
+    16 640 long chunks; exact cover, every length a forced cut or a tail, a sample vs the oracle,
+    and identical digests for identical chunks across buffers."""
+    prm = P(max_len=131072, pred_mask=0xFFFFFF)
+    e = engine_for(prm)
+    nbuf, L = 520, 4 * 2**20
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=L, records=False)
+    batch.fill_streams(first_stream=1200, bufs_per_stream=1)
+    v = batch.data.view(nbuf, L)
+    v[1::2].copy_(v[0::2])  # odd buffers copy even ones: their chunk lists must be identical
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    nlong = int(sum((ln[b, :counts[b]] > 32768).sum() for b in range(nbuf)))
+    assert nlong > 16384, nlong
+    _check_cover(counts, st, ln, L, prm)
+    for b in range(0, nbuf, 2):
+        c = counts[b]
+        assert counts[b + 1] == c and (st[b + 1, :c] == st[b, :c]).all() and (dg[b + 1, :c] == dg[b, :c]).all()
+    host = batch.data.view(nbuf, L)
+    for b in (0, 1, 257, 518):
+        buf = host[b].cpu().numpy()
+        es, el, ed = O.chunk(buf, O.Params(**prm))
+        c = counts[b]
+        assert st[b, :c].tolist() == es.tolist() and ln[b, :c].tolist() == el.tolist(), b
+        assert (dg[b, :c] == ed).all(), b
