@@ -725,3 +725,31 @@ def test_device_long_chunks_beyond_split_cap():
         c = counts[b]
         assert st[b, :c].tolist() == es.tolist() and ln[b, :c].tolist() == el.tolist(), b
         assert (dg[b, :c] == ed).all(), b
+
+
+def test_sectioned_mixed_joined_and_stitched_buffers():
+    """One batch of 5 MiB buffers (sectioned cut walk) where some buffers' sections all join in
+    parallel and others need the sequential stitch (all-zero data whose cuts never line up with
+    the sections; a 16-bit predicate's forced cuts out of phase): each buffer exactly as the oracle,
+    and the record table consistent with the slots (the histogram both passes feed)."""
+    prm = P(min_len=2999, max_len=131072)
+    L, nbuf = 5 * 2**20, 6
+    e = engine_for(prm)
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=L)
+    batch.fill_streams(first_stream=1300, bufs_per_stream=1)
+    v = batch.data.view(nbuf, L)
+    v[1].zero_()                      # never joins: falls back
+    v[4, 1_000_000:3_500_000].zero_()  # a zero run across two sections
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    host = v.cpu().numpy()
+    for b in range(nbuf):
+        es, el, ed = O.chunk(host[b], O.Params(**prm))
+        c = counts[b]
+        assert st[b, :c].tolist() == es.tolist() and ln[b, :c].tolist() == el.tolist(), b
+        assert (dg[b, :c] == ed).all(), b
+    recs = batch.record_table().cpu().numpy()
+    assert len(recs) == total
+    want = sorted(bytes(dg[b, i]) for b in range(nbuf) for i in range(counts[b]))
+    assert sorted(bytes(r[:32]) for r in recs) == want  # every chunk fingerprinted exactly once
