@@ -621,6 +621,125 @@ __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint3
     if (lane == 0) a.counts[b] = cnt < a.cap ? cnt : a.cap;
 }
 
+// First candidate position in [lo, hi] of uniform buffer b (buffer-relative), or -1, from the
+// scan's stored segment summaries (piece mode, ResolveArgs::seg_sum): lane l takes segment
+// lo / seg_len + l — its candidates are the summary's (the segment's first kSumCands) and, past
+// them, the sparse bitmap words the scan stored from the summary's overflow on.  One round covers
+// 64 segments (256 KiB at 4 KiB segments; a search spans at most max_len).
+__device__ __forceinline__ int64_t find_first_sum(const ResolveArgs& a, uint32_t b, uint32_t lo, uint32_t hi,
+                                                  uint32_t lane) {
+    const uint32_t sl = a.seg_len;
+    const uint64_t spb = a.uniform_len / sl;
+    const uint64_t word0 = ((uint64_t)b * a.uniform_len) >> 5;
+    for (uint32_t s0 = lo / sl; s0 <= hi / sl; s0 += 64) {
+        const uint32_t sj = s0 + lane;
+        uint32_t best = 0xFFFFFFFFu;
+        if (sj <= hi / sl) {
+            const uint32_t* ss = a.seg_sum + ((uint64_t)b * spb + sj) * kSegSumWords;
+            const uint4 q = *reinterpret_cast<const uint4*>(ss);
+            const uint32_t nc = ss[4], ovf = ss[5];
+            const uint32_t base = sj * sl;
+            const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t v = (qw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                const uint32_t c = base + v;
+                if (v != 0xFFFFu && c >= lo && c <= hi && c < best) best = c;
+            }
+            if (best == 0xFFFFFFFFu && nc > kSumCands) {
+                // the segment's later candidates, in the bitmap words stored from ovf on
+                uint32_t x = base + ovf > lo ? base + ovf : lo;
+                const uint32_t seg_hi = base + sl - 1;
+                const uint32_t to = seg_hi < hi ? seg_hi : hi;
+                while (x <= to) {
+                    uint32_t w = a.bitmap[word0 + (x >> 5)] >> (x & 31);
+                    const uint32_t span = to - x;
+                    if (span < 31) w &= (2u << span) - 1u;
+                    if (w) { best = x + __builtin_ctz(w); break; }
+                    x = (x | 31u) + 1u;
+                }
+            }
+        }
+        const uint64_t m = __ballot(best != 0xFFFFFFFFu);
+        if (m) return (int64_t)__builtin_amdgcn_readlane(best, (int)__builtin_ctzll(m));
+    }
+    return -1;
+}
+
+// Speculative walk of one 64-segment piece of a long buffer (the sectioned cut walk with
+// sections of 64 x seg_len bytes: one wave scanned exactly this piece), from the lanes' candidate
+// summaries instead of bitmap searches: chunk starts from an assumed start at the piece start,
+// each cut found inside the piece (or forced inside it); the walk stops at the first chunk whose
+// cut lies past the piece end — cdc_resolve_join_kernel finds that one in the complete bitmap and
+// writes spec_next.  Replaces cdc_resolve_spec_kernel's per-chunk bitmap round trips.
+__device__ __forceinline__ void piece_walk_from_summary(const ResolveArgs& a, uint32_t item, uint32_t r0, uint32_t lane,
+                                                        const uint32_t (&sm)[4], uint32_t ncand, uint32_t ovf_off,
+                                                        uint32_t seg_len, uint64_t word0) {
+    const uint32_t len = a.uniform_len;
+    const uint32_t r1 = r0 + 64 * seg_len < len ? r0 + 64 * seg_len : len;
+    const uint32_t my_base = r0 + lane * seg_len;
+    uint32_t q0 = sm[0], q1 = sm[1], q2 = sm[2], q3 = sm[3];
+    {
+        const uint32_t sh = kSumCands - (ncand < kSumCands ? ncand : kSumCands);
+        if (sh & 4) { q3 = q1; q2 = q0; q1 = 0xFFFFFFFFu; q0 = 0xFFFFFFFFu; }
+        if (sh & 2) { q3 = q2; q2 = q1; q1 = q0; q0 = 0xFFFFFFFFu; }
+        if (sh & 1) {
+            q3 = __builtin_amdgcn_alignbit(q3, q2, 16);
+            q2 = __builtin_amdgcn_alignbit(q2, q1, 16);
+            q1 = __builtin_amdgcn_alignbit(q1, q0, 16);
+            q0 = (q0 << 16) | 0xFFFFu;
+        }
+    }
+    auto head_of = [&](uint32_t top) { return (top >> 16) == 0xFFFFu ? 0xFFFFFFFFu : my_base + (top >> 16); };
+    uint32_t head = head_of(q3);
+    const bool ovf = ncand > kSumCands;
+    uint32_t* sp = a.spec_starts + (uint64_t)item * a.spec_cap;
+    uint32_t start = r0, cnt = 0;
+    while (start < r1) {
+        if (lane == 0 && cnt < a.spec_cap) sp[cnt] = start;
+        cnt++;
+        const uint32_t lo = start + a.first_off;
+        const uint32_t forced = start + a.max_len - 1;
+        const uint32_t hi = forced < len - 1 ? forced : len - 1;
+        const uint32_t hp = hi < r1 - 1 ? hi : r1 - 1;  // this piece's part of the search
+        int64_t k = -1;
+        if (lo <= hp) {
+            for (;;) {  // drop every candidate the walk has passed
+                const bool adv = head < lo;
+                if (__ballot(adv) == 0) break;
+                if (adv) {
+                    q3 = __builtin_amdgcn_alignbit(q3, q2, 16);
+                    q2 = __builtin_amdgcn_alignbit(q2, q1, 16);
+                    q1 = __builtin_amdgcn_alignbit(q1, q0, 16);
+                    q0 = (q0 << 16) | 0xFFFFu;
+                    head = head_of(q3);
+                }
+            }
+            uint32_t best = head <= hp ? head : 0xFFFFFFFFu;
+            if (ovf && head == 0xFFFFFFFFu) {
+                uint32_t x = my_base + ovf_off > lo ? my_base + ovf_off : lo;
+                const uint32_t seg_hi = my_base + seg_len - 1;
+                const uint32_t to = seg_hi < hp ? seg_hi : hp;
+                while (x <= to) {
+                    uint32_t w = a.bitmap[word0 + (x >> 5)] >> (x & 31);
+                    const uint32_t span = to - x;
+                    if (span < 31) w &= (2u << span) - 1u;
+                    if (w) { best = x + __builtin_ctz(w); break; }
+                    x = (x | 31u) + 1u;
+                }
+            }
+            const uint64_t m = __ballot(best != 0xFFFFFFFFu);
+            if (m) k = (int64_t)__builtin_amdgcn_readlane(best, (int)__builtin_ctzll(m));
+        }
+        if (k < 0) {
+            if (hi > r1 - 1) break;  // the cut lies past the piece: the join kernel finds it
+            k = (int64_t)hi;         // forced cut, or the buffer's tail chunk, inside the piece
+        }
+        start = (uint32_t)k + 1;
+    }
+    if (lane == 0) a.spec_cnt[item] = cnt < a.spec_cap ? cnt : a.spec_cap;
+}
+
 // Scan variants (DESIGN.md "Rabin scan"): C lane-private table copies (32: conflict-free,
 // 128 KiB, one 1024-thread workgroup per CU; 16: 2-way, 64 KiB, two workgroups per CU), NCH
 // independent segments per lane, BLK bytes per lane per iteration (128 = one whole cache line
@@ -716,7 +835,7 @@ __device__ __forceinline__ void scan_iter(const ScanArgs& a, const uint8_t* tab,
     // FUSE == 2 with the fused resolve: bitmap words are stored only once a lane's summary has
     // overflowed (> kSumCands candidates), from that block on; resolve_from_summary reads them
     // only there.  Saves the 0.5 GB of bitmap writes per 4 GiB.
-    const bool sparse_bm = CFG::kFuse == 2 && a.fuse_resolve;
+    const bool sparse_bm = CFG::kFuse == 2 && a.fuse_resolve != 0;
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
         if (nblk[c] != 0 && !first[c]) {
@@ -850,12 +969,32 @@ __device__ __forceinline__ void scan_iter(const ScanArgs& a, const uint8_t* tab,
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if constexpr (CFG::kFuse == 2) {
+                if (a.fuse_resolve == 2) {
+                    // piece mode (one chain only; the engine selects it for the production scan):
+                    // the wave's 64 segments are piece (seg0 mod spb) / 64 of buffer seg0 / spb (a
+                    // long uniform buffer, sections of 64 segments)
+                    if constexpr (NCH == 1) {
+                        if (base + tid < total) {  // this lane's segment summary, for the join / stitch
+                            uint32_t* ss = a.res.seg_sum + (base + tid) * kSegSumWords;
+                            *reinterpret_cast<uint4*>(ss) = make_uint4(sm[0][0], sm[0][1], sm[0][2], sm[0][3]);
+                            *reinterpret_cast<uint2*>(ss + 4) = make_uint2(ncand[0], ovf_off[0]);
+                        }
+                        const uint64_t spb = a.uniform_len / a.seg_len;
+                        const uint64_t b = seg0 / spb;
+                        const uint32_t piece = (uint32_t)((seg0 - b * spb) >> 6);
+                        if (seg0 < total)
+                            piece_walk_from_summary(a.res, (uint32_t)b * a.res.nsec + piece, piece * 64 * a.seg_len,
+                                                    lane, sm[0], ncand[0], ovf_off[0], a.seg_len,
+                                                    (b * a.uniform_len) >> 5);
+                    }
+                } else {
 #pragma unroll
-                for (int c = 0; c < NCH; c++) {
-                    const uint64_t sc = seg0 + (uint64_t)c * bdim;
-                    if (sc < total)
-                        resolve_from_summary<(CFG::kAbl & 128) == 0>(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c], ovf_off[c], a.seg_len,
-                                             lhist);
+                    for (int c = 0; c < NCH; c++) {
+                        const uint64_t sc = seg0 + (uint64_t)c * bdim;
+                        if (sc < total)
+                            resolve_from_summary<(CFG::kAbl & 128) == 0>(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c],
+                                                                         ovf_off[c], a.seg_len, lhist);
+                    }
                 }
             } else {
                 if (seg0 < total) resolve_buffer(a.res, (uint32_t)(seg0 >> 6), lane, lhist);

@@ -172,12 +172,14 @@ struct Workspace {
     DevBuf<uint32_t> tasks;
     DevBuf<uint32_t> spec_starts, spec_cnt, spec_next;  // sectioned cut walk of very long buffers
     DevBuf<uint32_t> join;  // its parallel stitch: kJoinWords per section, then one flag per buffer
+    DevBuf<uint32_t> seg_sum;  // piece mode: the scan's segment summaries (kSegSumWords per segment)
     DevBuf<uint32_t> x_scratch;  // extent ordering (getHash in bulk): hist | cursor | total, starts | tasks
     hipEvent_t free_ev = nullptr;
     bool pending = false;  // free_ev recorded and possibly not reached yet
     uint32_t* overflow() const { return small.p + 2 * kMaxBins; }
     void release_all() {
-        for (auto* b : {&bitmap, &small, &rec_base, &tasks, &spec_starts, &spec_cnt, &spec_next, &join, &x_scratch})
+        for (auto* b : {&bitmap, &small, &rec_base, &tasks, &spec_starts, &spec_cnt, &spec_next, &join, &seg_sum,
+                        &x_scratch})
             b->release();
         seg_prefix.release();
     }
@@ -247,7 +249,8 @@ struct DevEngine {
     bool small_seg = true;                   // short scan segments for small batches (tuning: SDFS_SMALL_SEG)
     bool long_split = true;                  // latency form for chunks > 32 KiB (tuning: SDFS_LONG_SPLIT)
     bool par_stitch = true;                  // parallel join/place of long buffers' sections (tuning: SDFS_PAR_STITCH)
-    uint32_t sec_log2 = 20;                  // section length of long buffers' cut walk (tuning: SDFS_SEC_LOG2)
+    uint32_t sec_log2 = 18;                  // section length of long buffers' cut walk (tuning: SDFS_SEC_LOG2)
+    bool piece_walk = true;                  // sections walked in the scan's epilogue when they fit (tuning: SDFS_PIECE_WALK)
     bool scan_prio = false;                  // pre-fingerprint stages on a high-priority stream (tuning: SDFS_SCAN_PRIO)
     hipStream_t s_scan = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -331,7 +334,8 @@ uint32_t slot_cap_for(const sdfs_cdc_params& p, uint64_t len) {
 
 // ---- workspace ring ----
 struct WsNeed {
-    uint64_t bitmap_words = 0, seg_prefix = 0, rec_base = 0, tasks = 0, spec_starts = 0, spec_items = 0, x_scratch = 0;
+    uint64_t bitmap_words = 0, seg_prefix = 0, rec_base = 0, tasks = 0, spec_starts = 0, spec_items = 0, x_scratch = 0,
+             seg_sum = 0;
 };
 
 // Next workspace of the ring (or `own`, a queue slot's), sized for `nd`, ordered behind its
@@ -344,7 +348,7 @@ int ws_acquire(DevEngine* e, const WsNeed& nd, hipStream_t s, Workspace** out, W
                       (!nd.spec_items || (w->spec_starts.fits(nd.spec_starts) && w->spec_cnt.fits(nd.spec_items) &&
                                           w->spec_next.fits(nd.spec_items) &&
                                           w->join.fits(nd.spec_items * kJoinWords + nd.rec_base))) &&
-                      (!nd.x_scratch || w->x_scratch.fits(nd.x_scratch));
+                      (!nd.x_scratch || w->x_scratch.fits(nd.x_scratch)) && (!nd.seg_sum || w->seg_sum.fits(nd.seg_sum));
     if (!fits && w->pending) HIP_TRY(hipEventSynchronize(w->free_ev));  // never free memory in use
     HIP_TRY(w->bitmap.ensure(std::max<uint64_t>(nd.bitmap_words, 2)));
     HIP_TRY(w->small.ensure(kSmall + 8));
@@ -358,6 +362,7 @@ int ws_acquire(DevEngine* e, const WsNeed& nd, hipStream_t s, Workspace** out, W
         HIP_TRY(w->join.ensure(nd.spec_items * kJoinWords + nd.rec_base));  // + one flag per buffer
     }
     if (nd.x_scratch) HIP_TRY(w->x_scratch.ensure(nd.x_scratch));
+    if (nd.seg_sum) HIP_TRY(w->seg_sum.ensure(nd.seg_sum));
     if (w->pending) HIP_TRY(hipStreamWaitEvent(s, w->free_ev, 0));
     *out = w;
     return SDFS_CDC_OK;
@@ -399,6 +404,8 @@ WsNeed pipeline_need(const DevEngine* e, uint64_t data_bytes, uint32_t nbuf, uin
         *spec_cap_out = sec / (e->first_off + 1) + 2;
         nd.spec_items = (uint64_t)nbuf * *nsec_out;
         nd.spec_starts = nd.spec_items * *spec_cap_out;
+        if (uniform_len)  // piece mode's segment summaries (run_pipeline decides; sized for it here)
+            nd.seg_sum = (uint64_t)nbuf * ((uniform_len + e->seg_len - 1) / e->seg_len) * kSegSumWords;
     }
     return nd;
 }
@@ -432,10 +439,13 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
         HIP_TRY(hipStreamWaitEvent(e->s_scan, e->ev_fork, 0));
         s = e->s_scan;
     }
-    // A batch of fewer buffers than SIMDs (a coalescing-queue pass) scans in short segments: the
-    // fused walk's one wave per buffer would leave most SIMDs idle and put a 4 KiB serial chain on
-    // every lane (0.18 ms); 512-byte segments plus the separate walk take ~0.07 ms.
-    const uint32_t seg_len = (nbuf < (uint32_t)e->num_cus * 4 && e->seg_len > kSmallBatchSeg &&
+    // A batch too small to give every SIMD a wave of full segments (a coalescing-queue pass:
+    // fewer 256 KiB buffers than SIMDs) scans in short segments: the fused walk's one wave per
+    // buffer would leave most SIMDs idle and put a 4 KiB serial chain on every lane (0.18 ms);
+    // 512-byte segments plus the separate walk take ~0.07 ms.  Counted in
+    // segments, not buffers: 102 backup buffers of 40 MiB are a million segments.
+    const uint64_t full_segs = data_bytes / e->seg_len;
+    const uint32_t seg_len = (full_segs < (uint64_t)e->num_cus * 4 * 64 && e->seg_len > kSmallBatchSeg &&
                               e->seg_len % kSmallBatchSeg == 0 && e->small_seg)
                                  ? kSmallBatchSeg
                                  : e->seg_len;
@@ -524,7 +534,17 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     // one wave = one buffer: the scan kernel resolves the cuts in its epilogue
     const bool fused = e->scan_info.fuse && uniform_len && (e->scan_info.chains == 1 || e->scan_info.fuse == 2) &&
                        (uint64_t)uniform_len == 64ull * seg_len && seg_len < 0xFFFFu;
-    sa.fuse_resolve = fused ? 1u : 0u;
+    // long uniform buffers whose sections are exactly one wave's 64 segments: the scan's epilogue
+    // walks every section speculatively from the lanes' summaries (no spec kernel)
+    const bool piece = !fused && e->piece_walk && e->par_stitch && sec_len && uniform_len && w->seg_sum.p &&
+                       e->scan_info.fuse == 2 && e->scan_info.chains == 1 &&
+                       sec_len == 64ull * seg_len && uniform_len % sec_len == 0 && seg_len < 0xFFFF;
+    if (piece) {
+        ra.spec_from_scan = 1;
+        ra.seg_sum = w->seg_sum.p;
+        ra.seg_len = seg_len;
+    }
+    sa.fuse_resolve = fused ? 1u : piece ? 2u : 0u;
     sa.res = ra;
     // One workgroup per CU (the LDS tables); a batch too small to give every CU 1024 threads
     // (fewer than ~4096 write buffers, e.g. the coalescing queue's) launches narrower
@@ -1192,6 +1212,7 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_SMALL_SEG")) e->small_seg = atoi(v) != 0;
     if (const char* v = getenv("SDFS_LONG_SPLIT")) e->long_split = atoi(v) != 0;
     if (const char* v = getenv("SDFS_PAR_STITCH")) e->par_stitch = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_PIECE_WALK")) e->piece_walk = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SEC_LOG2")) e->sec_log2 = (uint32_t)std::max(16, std::min(atoi(v), 24));
     if (const char* v = getenv("SDFS_SCAN_PRIO")) e->scan_prio = atoi(v) != 0;
     if (e->scan_prio) {

@@ -63,7 +63,16 @@ struct ResolveArgs {
     // then one flag per buffer (1 = the sequential stitch walks it)
     uint32_t* join;        // [nbuf * nsec * kJoinWords]
     uint32_t* join_bad;    // [nbuf]
+    // 1: the scan's epilogue walked every section (piece_walk_from_summary: spec_starts and
+    // spec_cnt, each section's last chunk open) — no spec kernel; the join kernel writes spec_next.
+    // The scan then stores the bitmap sparsely (from a segment's summary overflow on) and every
+    // segment's summary in seg_sum (kSegSumWords each, global segment order); the join and
+    // stitch kernels search candidates there (find_first_sum) instead of in the bitmap.
+    uint32_t spec_from_scan;
+    uint32_t* seg_sum;
+    uint32_t seg_len;
 };
+constexpr uint32_t kSegSumWords = 8;  // summary u16 x 8 (4 words) | ncand | ovf_off | pad
 constexpr uint32_t kJoinExtra = 8;  // true chunk starts a section may take before its chains meet
 constexpr uint32_t kJoinWords = 2 + kJoinExtra;
 // Section length of the sectioned cut walk for a buffer of `len` bytes (0 = not sectioned).

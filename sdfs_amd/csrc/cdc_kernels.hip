@@ -361,18 +361,42 @@ __global__ __launch_bounds__(256) void cdc_resolve_join_kernel(ResolveArgs a) {
         const uint32_t r0 = j * a.sec_len;
         uint32_t* jo = a.join + (uint64_t)item * kJoinWords;
         uint32_t m = 0, nx = 0;
+        const uint64_t word0 = off >> 5;
+        // one true step from chunk start p (the next chunk's start)
+        auto step = [&](uint32_t p) -> uint32_t {
+            const uint32_t lo = p + a.first_off;
+            const uint32_t forced = p + a.max_len - 1;
+            const uint32_t hi = forced < len - 1 ? forced : len - 1;
+            int64_t k = -1;
+            if (lo <= hi) k = a.seg_sum ? find_first_sum(a, b, lo, hi, lane) : find_first_wide(a.bitmap, word0, lo, hi, lane);
+            if (k < 0) k = (int64_t)hi;
+            return (uint32_t)k + 1;
+        };
+        // the scan's piece walk left every section's last chunk open: close this section's
+        // (spec_next) and recompute the previous section's from its last start — the same value
+        // that section's own wave writes, so no ordering between the waves is needed
+        uint32_t own_next = 0, prev_next = 0;
+        if (a.spec_from_scan) {
+            const uint32_t cm = a.spec_cnt[item];
+            own_next = r0 >= len || cm == 0 ? len : step(a.spec_starts[(uint64_t)item * a.spec_cap + cm - 1]);
+            if (lane == 0) a.spec_next[item] = own_next;
+            if (j > 0 && r0 < len) {
+                const uint32_t cp = a.spec_cnt[item - 1];
+                prev_next = cp == 0 ? len : step(a.spec_starts[(uint64_t)(item - 1) * a.spec_cap + cp - 1]);
+            }
+        }
         if (j > 0 && r0 < len) {
             const uint32_t r1 = min(r0 + a.sec_len, len);
             const uint32_t cm = a.spec_cnt[item];
             const uint32_t* sp = a.spec_starts + (uint64_t)item * a.spec_cap;
-            const uint64_t word0 = off >> 5;
-            uint32_t p = a.spec_next[item - 1];
+            const uint32_t snext = a.spec_from_scan ? own_next : a.spec_next[item];
+            uint32_t p = a.spec_from_scan ? prev_next : a.spec_next[item - 1];
             if (p >= len) {
                 m = cm;  // the chain ended before this section: none of its speculative starts is a cut
             } else {
                 for (;;) {
                     if (p >= r1) {  // passed through without meeting: fine if it leaves where they do
-                        m = p == a.spec_next[item] ? cm : kJoinUnmerged;
+                        m = p == snext ? cm : kJoinUnmerged;
                         break;
                     }
                     int32_t found = -1;
@@ -393,15 +417,9 @@ __global__ __launch_bounds__(256) void cdc_resolve_join_kernel(ResolveArgs a) {
                         m = kJoinUnmerged;
                         break;
                     }
-                    const uint32_t lo = p + a.first_off;
-                    const uint32_t forced = p + a.max_len - 1;
-                    const uint32_t hi = forced < len - 1 ? forced : len - 1;
-                    int64_t k = -1;
-                    if (lo <= hi) k = find_first_wide(a.bitmap, word0, lo, hi, lane);
-                    if (k < 0) k = (int64_t)hi;
                     if (lane == 0) jo[2 + nx] = p;
                     nx++;
-                    p = (uint32_t)k + 1;
+                    p = step(p);
                 }
             }
         }
@@ -544,7 +562,8 @@ __global__ __launch_bounds__(256) void cdc_resolve_stitch_kernel(ResolveArgs a) 
                 const uint32_t forced = p + a.max_len - 1;
                 const uint32_t hi = forced < len - 1 ? forced : len - 1;
                 int64_t k = -1;
-                if (lo <= hi) k = find_first_wide(a.bitmap, word0, lo, hi, lane);
+                if (lo <= hi)
+                    k = a.seg_sum ? find_first_sum(a, b, lo, hi, lane) : find_first_wide(a.bitmap, word0, lo, hi, lane);
                 if (k < 0) k = (int64_t)hi;
                 const uint32_t clen = (uint32_t)k + 1 - p;
                 if (cnt < a.cap) {
@@ -586,7 +605,7 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
         // very long buffers: speculative walk per section (one workgroup each), then stitch
         const uint64_t items = (uint64_t)a.nbuf * a.nsec;
         const uint32_t g = (uint32_t)std::min<uint64_t>((items + 3) / 4, 1u << 20);
-        hipLaunchKernelGGL(cdc_resolve_spec_kernel, dim3(g), dim3(256), 0, s, a);
+        if (!a.spec_from_scan) hipLaunchKernelGGL(cdc_resolve_spec_kernel, dim3(g), dim3(256), 0, s, a);
         if (a.join && a.join_bad) {
             hipLaunchKernelGGL(cdc_resolve_join_kernel, dim3(g), dim3(256), 0, s, a);
             hipLaunchKernelGGL(cdc_resolve_place_kernel, dim3(g), dim3(256), 0, s, a);
