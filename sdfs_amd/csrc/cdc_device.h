@@ -621,6 +621,179 @@ __device__ __forceinline__ void resolve_from_summary(const ResolveArgs& a, uint3
     if (lane == 0) a.counts[b] = cnt < a.cap ? cnt : a.cap;
 }
 
+// Cross-lane scans on the DPP network (VALU only: no trip through the LDS unit, whose queue the
+// scan's table lookups keep long).  Inclusive sum / max over the wave; wave_shr1: lane i gets
+// lane i - 1's value, lane 0 gets 0.
+#define SDFS_DPP(x, ctrl, rm) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x), (ctrl), (rm), 0xf, false))
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += SDFS_DPP(x, 0x111, 0xf);  // row_shr:1
+    x += SDFS_DPP(x, 0x112, 0xf);  // row_shr:2
+    x += SDFS_DPP(x, 0x114, 0xf);  // row_shr:4
+    x += SDFS_DPP(x, 0x118, 0xf);  // row_shr:8
+    x += SDFS_DPP(x, 0x142, 0xa);  // row_bcast:15 into rows 1 and 3
+    x += SDFS_DPP(x, 0x143, 0xc);  // row_bcast:31 into rows 2 and 3
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    auto mx = [](uint32_t u, uint32_t v) { return u > v ? u : v; };
+    x = mx(x, SDFS_DPP(x, 0x111, 0xf));
+    x = mx(x, SDFS_DPP(x, 0x112, 0xf));
+    x = mx(x, SDFS_DPP(x, 0x114, 0xf));
+    x = mx(x, SDFS_DPP(x, 0x118, 0xf));
+    x = mx(x, SDFS_DPP(x, 0x142, 0xa));
+    x = mx(x, SDFS_DPP(x, 0x143, 0xc));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return SDFS_DPP(x, 0x138, 0xf); }
+#undef SDFS_DPP
+
+// List walk (production since round 4): the greedy cut walk of buffer b from the lanes' candidate
+// summaries with only four trips through the LDS unit, so it does not queue behind the other
+// waves' table lookups once per cut as the queue walk's lane-0 work and an LDS pointer chase
+// would (scripts/probe_r4_walk_pmc.sh, probe_r4_list_walk.sh):
+//   1. the lanes' candidates, ascending, go to the wave's LDS list at the (DPP) prefix of their
+//      counts; entry e (page e / 64) is then read back by lane e % 64;
+//   2. each entry's next-cut pointer — the first entry >= pos + 1 + first_off, if within the
+//      chunk's max_len — from the segment lane T holding pos + 1 + first_off: its list base and
+//      count (one bpermute) and its <= 8 entries plus the one after (one round of reads);
+//   3. the chain from the first cut follows the pointers with v_readlane (registers only) and
+//      marks the cut entries in per-page SGPR masks;
+//   4. every lane writes the chunk of its marked entry (rank from the masks, start = the previous
+//      cut + 1 by a DPP max-scan) and lane 0 the tail chunk.
+// It declines (false, nothing written) when a summary overflowed, the list would exceed kListCap,
+// seg_len is not a power of two, or a forced cut (a max_len chunk ending at a non-candidate)
+// occurs before the tail; the queue walk (resolve_from_summary) then resolves the buffer.
+constexpr uint32_t kListCap = 256;
+
+__device__ __forceinline__ bool resolve_from_list(const ResolveArgs& a, uint32_t b, uint32_t lane,
+                                                  const uint32_t (&sm)[4], uint32_t ncand, uint32_t seg_len,
+                                                  uint32_t* lhist, uint32_t* wl, uint32_t probe = 0) {
+    // probe (measurement only, tuning: SDFS_SKIP_WALK=2/3): 2 = no outputs at all, 3 = chunk
+    // stores and LDS histogram but no counts (the pipeline then sees no chunks)
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    const uint32_t len = a.uniform_len;
+    if (__ballot(ncand > kSumCands) || len > (1u << 22) || (seg_len & (seg_len - 1)) != 0) return false;
+    const uint32_t n = ncand;
+    const uint32_t incl = wave_incl_sum(n);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    if (total > kListCap) return false;
+    const uint32_t base = incl - n;
+    const uint32_t sh = __builtin_ctz(seg_len);
+    // 1. the sorted list (summary slot j, j = 0 the newest = largest, goes to base + n - 1 - j)
+#pragma unroll
+    for (uint32_t j = 0; j < kSumCands; j++)
+        if (j < n) wl[base + n - 1 - j] = (lane << sh) + ((sm[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr uint32_t NP = kListCap / 64;
+    uint32_t pos[NP], np[NP];
+#pragma unroll
+    for (uint32_t k = 0; k < NP; k++) pos[k] = lane + 64 * k < total ? wl[lane + 64 * k] : kNone;
+    // 2. next pointers: entries of lane T's segment sit at [base_T, base_T + n_T); the first entry
+    //    >= lo is base_T + (those < lo), and it is the one read at j = that count (entries of later
+    //    segments all exceed lo)
+    const uint32_t bn = base | (n << 16);
+#pragma unroll
+    for (uint32_t k = 0; k < NP; k++) {
+        np[k] = kNone;
+        if (64 * k < total) {
+            const uint32_t p = pos[k];
+            const uint32_t lo = p + 1 + a.first_off;
+            const uint32_t hi = p + a.max_len < len - 1 ? p + a.max_len : len - 1;
+            const bool act = p != kNone && lo <= hi;
+            const uint32_t t = act ? lo >> sh : 0u;
+            const uint32_t tb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t << 2), (int)bn);
+            const uint32_t tbase = tb & 0xFFFFu, tn = tb >> 16;
+            uint32_t less = 0, q = kNone;
+#pragma unroll
+            for (uint32_t j = 0; j <= kSumCands; j++) {
+                const uint32_t e = tbase + j;
+                const uint32_t v = act && j <= tn && e < total ? wl[e] : kNone;
+                less += v < lo ? 1u : 0u;
+                q = v >= lo && v < q ? v : q;
+            }
+            if (act && q <= hi) np[k] = tbase + less;
+        }
+    }
+    // 3. the chain (wave-uniform): the first cut is the first entry >= first_off, if within max_len
+    uint32_t first = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NP; k++) first += (uint32_t)__builtin_popcountll(__ballot(pos[k] < a.first_off));
+    uint32_t idx = kNone;
+    if (first < total) {
+        uint32_t fp = kNone;
+#pragma unroll
+        for (uint32_t k = 0; k < NP; k++)
+            if ((first >> 6) == k) fp = __builtin_amdgcn_readlane(pos[k], first & 63);
+        const uint32_t hi0 = a.max_len - 1 < len - 1 ? a.max_len - 1 : len - 1;
+        if (fp <= hi0) idx = first;
+    }
+    uint64_t cut[NP];
+    uint32_t cnt = 0, start = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NP; k++) {
+        cut[k] = 0;
+        uint32_t last = kNone;
+        while (idx != kNone && (idx >> 6) == k) {
+            cut[k] |= 1ull << (idx & 63);
+            last = idx & 63;
+            cnt++;
+            idx = __builtin_amdgcn_readlane(np[k], last);
+        }
+        if (last != kNone) start = __builtin_amdgcn_readlane(pos[k], last) + 1;
+    }
+    // no candidate in the next chunk's range: the tail chunk if that range reaches the buffer end,
+    // else a forced cut — declined
+    if (start < len && start + a.max_len - 1 < len - 1) return false;
+    // 4. the chunks, wave-parallel
+    uint32_t carry_rank = 0, carry_pos = 0;  // cuts of the earlier pages, the last cut's end + 1
+#pragma unroll
+    for (uint32_t k = 0; k < NP; k++) {
+        if (cut[k] == 0) continue;
+        const bool c = (cut[k] >> lane) & 1;
+        const uint32_t rank = carry_rank + __builtin_amdgcn_mbcnt_hi((uint32_t)(cut[k] >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)cut[k], 0u));
+        const uint32_t end1 = c ? pos[k] + 1 : 0u;
+        uint32_t prev = wave_incl_max(wave_shr1(end1));
+        prev = prev > carry_pos ? prev : carry_pos;
+        if (c && probe != 2) {
+            if (rank < a.cap) {
+                const uint64_t slot = (uint64_t)b * a.cap + rank;
+                const uint32_t clen = end1 - prev;
+                a.starts[slot] = prev;
+                a.clens[slot] = clen;
+                uint32_t bin = sha_blocks(clen) >> a.bin_shift;
+                bin = bin < a.nbins ? bin : a.nbins - 1;
+                atomicAdd(&lhist[bin], 1u);
+            } else {
+                atomicOr(a.overflow, 1u);
+            }
+        }
+        carry_rank += (uint32_t)__builtin_popcountll(cut[k]);
+        const uint32_t mx = __builtin_amdgcn_readlane(wave_incl_max(end1), 63);
+        carry_pos = mx > carry_pos ? mx : carry_pos;
+    }
+    if (lane == 0 && probe) {
+        a.counts[b] = 0;
+    } else if (lane == 0) {
+        const uint32_t nchunks = cnt + (start < len ? 1u : 0u);
+        if (start < len) {  // the tail chunk
+            if (cnt < a.cap) {
+                const uint64_t slot = (uint64_t)b * a.cap + cnt;
+                a.starts[slot] = start;
+                a.clens[slot] = len - start;
+                uint32_t bin = sha_blocks(len - start) >> a.bin_shift;
+                bin = bin < a.nbins ? bin : a.nbins - 1;
+                atomicAdd(&lhist[bin], 1u);
+            } else {
+                atomicOr(a.overflow, 1u);
+            }
+        }
+        a.counts[b] = nchunks < a.cap ? nchunks : a.cap;
+    }
+    return true;
+}
+
 // First candidate position in [lo, hi] of uniform buffer b (buffer-relative), or -1, from the
 // scan's stored segment summaries (piece mode, ResolveArgs::seg_sum): lane l takes segment
 // lo / seg_len + l — its candidates are the summary's (the segment's first kSumCands) and, past
@@ -767,6 +940,8 @@ struct ScanCfg {
     static constexpr int kLds = scan_lds_bytes(C);
     static constexpr uint32_t kPushOff = C == 32 ? 0x10000u : 0x80u;
     static constexpr int kBlk = BLK;
+    // the list walk's per-wave LDS list (1 KiB per wave): one chain, the 32-copy tables
+    static constexpr bool kListWalk = kFuse == 2 && NCH == 1 && C == 32;
 };
 
 // One pass of the scan over the segments base + c * bdim + tid (c < chains) — one lane's share of
@@ -776,7 +951,8 @@ struct ScanCfg {
 template <int W, int PK, class CFG>
 __device__ __forceinline__ void scan_iter(const ScanArgs& a, const uint8_t* tab, uint32_t* lhist, uint64_t base,
                                           uint32_t tid, uint32_t bdim, uint64_t total, uint32_t lane, uint32_t c8,
-                                          uint32_t push_base, uint32_t& pa_reg, uint32_t& qa_reg) {
+                                          uint32_t push_base, uint32_t& pa_reg, uint32_t& qa_reg,
+                                          uint32_t* wlist = nullptr) {
     constexpr int MB =
         (CFG::kMirror ? kAblMirror : 0) | (CFG::kAbl & (kAblSgprPred | kAblSdwa | kAblSdwaPop | kAblMinGroup | kAblMinGroup8 | kAblPopSwap | kAblPopMux));
     constexpr int NCH = CFG::kChains;
@@ -962,7 +1138,7 @@ __device__ __forceinline__ void scan_iter(const ScanArgs& a, const uint8_t* tab,
         }
     }
     if constexpr (CFG::kFuse != 0) {
-        if (a.fuse_resolve) {
+        if (a.fuse_resolve && a.skip_walk != 1) {
             // this wave's 64 segments are buffer seg0 / 64: make the lanes' bitmap stores
             // visible to the whole wave (same CU, so no L1 staleness), then walk its cuts
             const uint64_t seg0 = base + (tid & ~63u);
@@ -991,9 +1167,18 @@ __device__ __forceinline__ void scan_iter(const ScanArgs& a, const uint8_t* tab,
 #pragma unroll
                     for (int c = 0; c < NCH; c++) {
                         const uint64_t sc = seg0 + (uint64_t)c * bdim;
-                        if (sc < total)
-                            resolve_from_summary<(CFG::kAbl & 128) == 0>(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c],
-                                                                         ovf_off[c], a.seg_len, lhist);
+                        if (sc < total) {
+                            bool done = false;
+                            if constexpr (CFG::kListWalk)
+                                if (wlist && a.list_walk)
+                                    done = resolve_from_list(a.res, (uint32_t)(sc >> 6), lane, sm[c], ncand[c], a.seg_len,
+                                                             lhist, wlist, a.skip_walk);
+                            if (!done && a.skip_walk > 1) {
+                                if (lane == 0) a.res.counts[(uint32_t)(sc >> 6)] = 0;
+                            } else if (!done)
+                                resolve_from_summary<(CFG::kAbl & 128) == 0>(a.res, (uint32_t)(sc >> 6), lane, sm[c],
+                                                                             ncand[c], ovf_off[c], a.seg_len, lhist);
+                        }
                     }
                 }
             } else {
@@ -1011,6 +1196,7 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
     constexpr int C = CFG::kCopies;
     __shared__ __attribute__((aligned(16))) uint8_t tab[CFG::kLds];
     __shared__ uint32_t lhist[CFG::kFuse ? kMaxBins : 1];  // fused resolve: chunk-length histogram
+    __shared__ uint32_t wlist[CFG::kListWalk ? CFG::kThreads / 64 * kListCap : 1];  // list walk: per wave
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.tab_image);
         uint4* dst = reinterpret_cast<uint4*>(tab);
@@ -1032,10 +1218,11 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
     const uint64_t per_iter = (uint64_t)blockDim.x * NCH;
 
     for (uint64_t base = (uint64_t)blockIdx.x * per_iter; base < total; base += (uint64_t)gridDim.x * per_iter) {
-        scan_iter<W, PK, CFG>(a, tab, lhist, base, threadIdx.x, blockDim.x, total, lane, c8, push_base, pa_reg, qa_reg);
+        scan_iter<W, PK, CFG>(a, tab, lhist, base, threadIdx.x, blockDim.x, total, lane, c8, push_base, pa_reg, qa_reg,
+                              CFG::kListWalk ? wlist + (threadIdx.x >> 6) * kListCap : nullptr);
     }
     if constexpr (CFG::kFuse != 0) {
-        if (a.fuse_resolve) {
+        if (a.fuse_resolve && a.skip_walk < 2) {
             __syncthreads();
             for (uint32_t i = threadIdx.x; i < a.res.nbins; i += blockDim.x)
                 if (lhist[i]) atomicAdd(&a.res.hist[i], lhist[i]);

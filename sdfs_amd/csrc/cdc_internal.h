@@ -99,6 +99,8 @@ struct ScanArgs {
     // right after scanning it, from its own L2-resident bitmap words (no separate resolve pass)
     uint32_t fuse_resolve;
     ResolveArgs res;
+    uint32_t skip_walk;  // measurement only (tuning: SDFS_SKIP_WALK): 1 no epilogue walk, 2/3 list walk without outputs
+    uint32_t list_walk;  // fused walk (fuse_resolve 1): the LDS list walk, else the queue walk only
 };
 // Every segment of the batch is a whole number of `blk`-byte blocks (the scan kernel's
 // kAblFullBlocks form may run it).

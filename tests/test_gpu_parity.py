@@ -753,3 +753,55 @@ def test_sectioned_mixed_joined_and_stitched_buffers():
     assert len(recs) == total
     want = sorted(bytes(dg[b, i]) for b in range(nbuf) for i in range(counts[b]))
     assert sorted(bytes(r[:32]) for r in recs) == want  # every chunk fingerprinted exactly once
+
+
+def _list_walk_buffers(nbuf: int, buf_len: int, seed: int) -> np.ndarray:
+    """Random buffers with constant-byte stretches (a constant window is not a candidate, so the
+    walk meets max_len chunks ending at non-candidates there) of varying length and place: none,
+    one short, one longer than max_len mid-buffer, one running to the buffer end, several."""
+    rng = np.random.default_rng(seed)
+    host = rng.integers(0, 256, nbuf * buf_len, dtype=np.uint8).reshape(nbuf, buf_len)
+    for b in range(nbuf):
+        kind = b % 5
+        if kind == 1:
+            o = int(rng.integers(0, buf_len - 8192))
+            host[b, o:o + int(rng.integers(100, 8000))] = 0x5A
+        elif kind == 2:
+            o = int(rng.integers(0, buf_len // 2))
+            host[b, o:o + int(rng.integers(70000, 120000))] = 0xA5
+        elif kind == 3:
+            host[b, buf_len - int(rng.integers(1000, 90000)):] = 0x33
+        elif kind == 4:
+            for _ in range(6):
+                o = int(rng.integers(0, buf_len - 40000))
+                host[b, o:o + int(rng.integers(2000, 40000))] = 0x77
+    return host
+
+
+@pytest.mark.parametrize("prm", [
+    P(),                                                  # the reference default mix
+    P(min_len=2047, pred_mask=0x7FF),                     # the metric's 4 KiB-mean mix
+    P(min_len=10239, pred_mask=0x7FF, max_len=65536),     # minLen spans several scan segments
+    P(min_len=511, pred_mask=0x3FF, max_len=6000),        # ~256 candidates per buffer: list full or over
+    P(min_len=2047, pred_mask=0x1FFF, max_len=8192),      # max_len chunks at non-candidates everywhere
+], ids=["default", "mix4k", "long_min", "list_cap", "forced"])
+def test_fused_list_walk_edges(prm):
+    """The fused walk's list form (scan epilogue, uniform 256 KiB buffers) and its fall-back to the
+    queue walk (summary overflow, > 256 candidates per buffer, forced cuts), buffer by buffer
+    against the oracle.  1024 buffers: smaller batches scan in short segments, without the fused
+    walk."""
+    e = engine_for(prm)
+    nbuf, buf_len = 1024, 262144
+    host = _list_walk_buffers(nbuf, buf_len, seed=len(str(prm)))
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=buf_len)
+    batch.data.copy_(torch.from_numpy(host.reshape(-1)))
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == counts.sum()
+    dl = O.Params(**prm).digest_len
+    for b in range(nbuf):
+        es, el, ed = O.chunk(host[b].tobytes(), O.Params(**prm))
+        c = counts[b]
+        assert c == len(es), b
+        assert st[b, :c].tolist() == es.tolist() and ln[b, :c].tolist() == el.tolist(), b
+        assert (dg[b, :c, :dl] == ed).all(), b
