@@ -135,3 +135,12 @@ def test_overflow_and_capacity_decline():
     ok = spread[:256]
     got = list_walk(ok, n, p_)
     assert got is None or got == greedy(ok, n, p_)
+
+
+def test_constants_match_the_kernel_header():
+    """The restatement's capacities are the kernel's (cdc_device.h)."""
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(__file__), "..", "sdfs_amd", "csrc", "cdc_device.h")).read()
+    assert int(re.search(r"constexpr uint32_t kListCap = (\d+);", src).group(1)) == LIST_CAP
+    assert int(re.search(r"constexpr uint32_t kSumCands = (\d+);", src).group(1)) == SUM_CANDS
