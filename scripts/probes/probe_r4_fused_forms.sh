@@ -3,7 +3,7 @@
 # 2 / 3 / 4; form 1 = two, interleaved) against production (scan + fingerprint kernels), and the
 # fingerprint kernel's line re-fetch bound at the 4 KiB-mean mix (hash variant 10 reads every
 # chunk from its start rounded down to 128 B: wrong digests, the traffic a fix could save).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 export SDFS_CDC_LIB=$PWD/sdfs_amd/libsdfs_cdc_tuning.so
 C='prod:;f1:SDFS_FUSED_PROBE=1;f2:SDFS_FUSED_PROBE=2;f3:SDFS_FUSED_PROBE=3;f4:SDFS_FUSED_PROBE=4'
 H='prod:;aligned:SDFS_HASH_VARIANT=10'

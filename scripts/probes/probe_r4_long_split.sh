@@ -3,7 +3,7 @@
 # form (chunk_hash_long_kernel; off: SDFS_LONG_SPLIT=0) and the parallel join/place stitch of the
 # sections (off: SDFS_PAR_STITCH=0), each against production, one process, interleaved; then the
 # configs[4] bench on the product library and a rocprof of it.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 bash scripts/gpu_session.sh \
  "long_split_ab:240:SDFS_CDC_LIB=$PWD/sdfs_amd/libsdfs_cdc_tuning.so CONFIGS='prod:;nolong:SDFS_LONG_SPLIT=0;seqstitch:SDFS_PAR_STITCH=0;neither:SDFS_LONG_SPLIT=0,SDFS_PAR_STITCH=0' ROUNDS=10 BACKUP=1 python3 scripts/ab.py" \
  "cfg_backup:300:CONFIG=backup python3 scripts/config_bench.py"

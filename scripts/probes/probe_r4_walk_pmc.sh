@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: instruction counts of the scan kernel with the list walk, the queue walk and no walk
 # (one PMC pass each, ab.py at the 4 KiB-mean mix, one config per run).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 R=$PWD
 export TMPDIR=/tmp SDFS_CDC_LIB=$R/sdfs_amd/libsdfs_cdc_tuning.so ROUNDS=2 MIN_SEG_KIB=2 MASK_BITS=11
 OUT=$R/gpurun_out/walk_pmc

@@ -650,7 +650,7 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return SDFS_DPP(x, 0
 // List walk (production since round 4): the greedy cut walk of buffer b from the lanes' candidate
 // summaries with only four trips through the LDS unit, so it does not queue behind the other
 // waves' table lookups once per cut as the queue walk's lane-0 work and an LDS pointer chase
-// would (scripts/probe_r4_walk_pmc.sh, probe_r4_list_walk.sh):
+// would (scripts/probes/probe_r4_walk_pmc.sh, probe_r4_list_walk.sh):
 //   1. the lanes' candidates, ascending, go to the wave's LDS list at the (DPP) prefix of their
 //      counts; entry e (page e / 64) is then read back by lane e % 64;
 //   2. each entry's next-cut pointer — the first entry >= pos + 1 + first_off, if within the
