@@ -18,7 +18,7 @@ from collections import defaultdict
 
 SHORT = {"cdc_scan_kernel": "scan", "chunk_hash_kernel": "hash", "cdc_prefix_kernel": "prefix",
          "cdc_scatter_kernel": "scatter", "fillBufferAligned": "memset", "seg_prefix_kernel": "seg_prefix",
-         "cdc_resolve": "resolve"}
+         "cdc_resolve": "resolve", "chunk_hash_long_kernel": "hash_long"}
 
 
 def short(name: str) -> str:

@@ -43,7 +43,7 @@ def main():
     out = {"source": os.path.relpath(f), "grbm_overhead_cycles_summed": over, "kernels": {}}
     for name, rows in by.items():
         rows = rows[a.skip:] or rows
-        if name not in ("scan", "hash"):
+        if name not in ("scan", "hash", "hash_long"):
             continue
         cyc = statistics.mean((r["GRBM_GUI_ACTIVE"] - over) / XCDS for r in rows)
         ns = statistics.mean(r["ns"] for r in rows)
