@@ -1217,9 +1217,37 @@ __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_ke
     // fused walk); small batches launch narrow workgroups so their waves do not share SIMDs
     const uint64_t per_iter = (uint64_t)blockDim.x * NCH;
 
-    for (uint64_t base = (uint64_t)blockIdx.x * per_iter; base < total; base += (uint64_t)gridDim.x * per_iter) {
-        scan_iter<W, PK, CFG>(a, tab, lhist, base, threadIdx.x, blockDim.x, total, lane, c8, push_base, pa_reg, qa_reg,
-                              CFG::kListWalk ? wlist + (threadIdx.x >> 6) * kListCap : nullptr);
+    uint32_t* const wl = CFG::kListWalk ? wlist + (threadIdx.x >> 6) * kListCap : nullptr;
+    // Work queue (tuning only, SDFS_SCAN_DYN=1; one-chain forms with a counter): each wave takes
+    // the next 64 segments (one 256 KiB buffer of the fused walk) from a per-launch counter, so
+    // waves that start late — their CU still running the other batch's fingerprint workgroups or
+    // an RCCL kernel — would take fewer items instead of stretching the launch; every wave leaves
+    // once the counter passes the last item.  Measured no faster at N = 1 and 2-5 % slower for
+    // the scan alone, so production keeps the static workgroup stride.  One call
+    // site, so the byte loop is compiled once.
+    bool dyn = false;
+    if constexpr (NCH == 1) dyn = a.wave_ctr != nullptr;
+    const uint32_t items = (uint32_t)((total + 63) >> 6);
+    uint64_t sbase = (uint64_t)blockIdx.x * per_iter;
+    for (;;) {
+        uint64_t base;
+        uint32_t tid, bdim;
+        if (dyn) {
+            uint32_t it = 0;
+            if (lane == 0) it = atomicAdd(a.wave_ctr, 1u);
+            it = __builtin_amdgcn_readfirstlane(it);
+            if (it >= items) break;
+            base = (uint64_t)it * 64;
+            tid = lane;
+            bdim = 64;
+        } else {
+            if (sbase >= total) break;
+            base = sbase;
+            tid = threadIdx.x;
+            bdim = blockDim.x;
+            sbase += (uint64_t)gridDim.x * per_iter;
+        }
+        scan_iter<W, PK, CFG>(a, tab, lhist, base, tid, bdim, total, lane, c8, push_base, pa_reg, qa_reg, wl);
     }
     if constexpr (CFG::kFuse != 0) {
         if (a.fuse_resolve && a.skip_walk < 2) {

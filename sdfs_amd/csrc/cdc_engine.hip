@@ -252,6 +252,7 @@ struct DevEngine {
     uint32_t sec_log2 = 18;                  // section length of long buffers' cut walk (tuning: SDFS_SEC_LOG2)
     uint32_t skip_walk = 0;                  // measurement only (tuning: SDFS_SKIP_WALK 1..3): no chunks
     bool list_walk = true;                   // fused walk: LDS list form (tuning: SDFS_LIST_WALK=0 = queue walk)
+    bool scan_dyn = false;                   // scan work queue per wave (tuning: SDFS_SCAN_DYN=1; slower)
     bool piece_walk = true;                  // sections walked in the scan's epilogue when they fit (tuning: SDFS_PIECE_WALK)
     bool scan_prio = false;                  // pre-fingerprint stages on a high-priority stream (tuning: SDFS_SCAN_PRIO)
     hipStream_t s_scan = nullptr;
@@ -549,6 +550,7 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     sa.fuse_resolve = fused ? 1u : piece ? 2u : 0u;
     sa.skip_walk = e->skip_walk;
     sa.list_walk = e->list_walk ? 1u : 0u;
+    sa.wave_ctr = e->scan_dyn ? w->small.p + 2 * kMaxBins + 8 : nullptr;  // zeroed with `small` above
     sa.res = ra;
     // One workgroup per CU (the LDS tables); a batch too small to give every CU 1024 threads
     // (fewer than ~4096 write buffers, e.g. the coalescing queue's) launches narrower
@@ -1219,6 +1221,7 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_PIECE_WALK")) e->piece_walk = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SKIP_WALK")) e->skip_walk = (uint32_t)std::max(0, std::min(atoi(v), 3));
     if (const char* v = getenv("SDFS_LIST_WALK")) e->list_walk = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SCAN_DYN")) e->scan_dyn = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SEC_LOG2")) e->sec_log2 = (uint32_t)std::max(16, std::min(atoi(v), 24));
     if (const char* v = getenv("SDFS_SCAN_PRIO")) e->scan_prio = atoi(v) != 0;
     if (e->scan_prio) {

@@ -101,6 +101,8 @@ struct ScanArgs {
     ResolveArgs res;
     uint32_t skip_walk;  // measurement only (tuning: SDFS_SKIP_WALK): 1 no epilogue walk, 2/3 list walk without outputs
     uint32_t list_walk;  // fused walk (fuse_resolve 1): the LDS list walk, else the queue walk only
+    uint32_t* wave_ctr;  // nullable, zeroed per launch: one-chain scans hand out 64-segment wave items
+                         // from this counter instead of a static workgroup stride
 };
 // Every segment of the batch is a whole number of `blk`-byte blocks (the scan kernel's
 // kAblFullBlocks form may run it).
