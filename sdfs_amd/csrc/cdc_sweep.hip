@@ -303,6 +303,10 @@ hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant,
     case 15: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true, 5>), dim3(blocks), dim3(256), 0, s, a); break;
     case 16: hipLaunchKernelGGL((chunk_hash_kernel<0, 8, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
     case 10: hipLaunchKernelGGL((chunk_hash_kernel<0, 4, 256, true, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 45:  // production kernel without its data loads (ABL bit 1: message words from the state;
+              // wrong digests): the clock of the same VALU work without the HBM traffic
+        hipLaunchKernelGGL((chunk_hash_kernel<0, 16 | 1, 256, true, true>), dim3(blocks), dim3(256), 0, s, a);
+        break;
     case 31:  // production kernel without the issue priority for waves of long chunks
         hipLaunchKernelGGL((chunk_hash_kernel<0, 16, 256, true, false>), dim3(blocks), dim3(256), 0, s, a);
         break;
