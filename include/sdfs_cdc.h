@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SDFS_CDC_ABI_VERSION 2
+#define SDFS_CDC_ABI_VERSION 3
 
 enum sdfs_cdc_status {
     SDFS_CDC_OK = 0,
@@ -85,7 +85,19 @@ typedef struct sdfs_cdc_params {
     uint32_t flags;         /* SDFS_CDC_FLAG_*; 0 = defaults */
     uint64_t max_batch_bytes; /* host-batch staging per slot (pinned, two slots); 0 = default 256 MiB */
     uint64_t device_mask;   /* ABI 2: bit i = HIP ordinal i in the device set (0 = use `device`) */
+    /* ABI 3: the FORM of the boundary predicate.  BoundaryDetectors.DEFAULT_BOUNDARY_DETECTOR
+     * (VariableSha256HashEngine.java:42, absent rabinwindow jar) is one of two detector forms
+     * (SURVEY.md A.3): a bitmask detector (fp & pred_mask) == pred_value (SDFS_CDC_PRED_MASK, the
+     * default) or a divisor detector fp % pred_div == pred_rem (SDFS_CDC_PRED_DIV; Java long
+     * remainder of the non-negative window fp).  pred_div >= 1; a power of two runs as the
+     * equivalent mask; any other divisor needs deg(poly) <= 53 (the default poly's degree). */
+    uint32_t pred_kind;     /* enum sdfs_cdc_pred_kind */
+    uint32_t reserved2;     /* 0 */
+    uint64_t pred_div;      /* SDFS_CDC_PRED_DIV: divisor D (1 .. 2^32-1) */
+    uint64_t pred_rem;      /* SDFS_CDC_PRED_DIV: target remainder R (R >= D never matches) */
 } sdfs_cdc_params;
+
+enum sdfs_cdc_pred_kind { SDFS_CDC_PRED_MASK = 0, SDFS_CDC_PRED_DIV = 1 };
 
 /* flags: serve every getChunks / getHash call with its own GPU round trip instead of coalescing
  * concurrent callers (A/B measurements; the results are identical). */

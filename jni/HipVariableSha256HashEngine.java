@@ -34,9 +34,22 @@ public final class HipVariableSha256HashEngine implements AbstractHashEngine {
      *  "sdfs.hip.device" set: -1 = every gfx950 device, the default; an ordinal = that GPU). */
     public HipVariableSha256HashEngine(HASHTYPE ht) throws IOException {
         int algo = ht == HASHTYPE.HASH256 ? 0 : (ht == HASHTYPE.HASH160 ? 1 : 2);  // SDFS_CDC_*
+        long[] det = boundaryDetector(System.getProperty("sdfs.hip.boundary", "mask:0xfff:0"));
         handle = nativeCreate(POLY, HashFunctionPool.bytesPerWindow, HashFunctionPool.minLen,
-                HashFunctionPool.maxLen, Main.CHUNK_LENGTH, algo, Integer.getInteger("sdfs.hip.device", -1));
+                HashFunctionPool.maxLen, Main.CHUNK_LENGTH, algo, Integer.getInteger("sdfs.hip.device", -1),
+                (int) det[0], det[1], det[2]);
         hashLen = nativeDigestLen(handle);
+    }
+
+    /** The form of BoundaryDetectors.DEFAULT_BOUNDARY_DETECTOR (VariableSha256HashEngine.java:42),
+     *  which the rabinwindow jar fixes and SDFS does not configure: "mask:M:V" is the bitmask
+     *  detector (fp &amp; M) == V, "div:D:R" the divisor detector fp % D == R (numbers decimal or 0x hex).
+     *  tools/java/JarParity.java tells which one (and which constants) a given jar uses. */
+    static long[] boundaryDetector(String spec) throws IOException {
+        String[] f = spec.trim().split(":");
+        if (f.length != 3 || !(f[0].equals("mask") || f[0].equals("div")))
+            throw new IOException("sdfs.hip.boundary must be mask:M:V or div:D:R, got " + spec);
+        return new long[] {f[0].equals("div") ? 1 : 0, Long.decode(f[1]), Long.decode(f[2])};
     }
 
     @Override public boolean isVariableLength() { return true; }
@@ -92,7 +105,8 @@ public final class HipVariableSha256HashEngine implements AbstractHashEngine {
     public static void register(java.nio.ByteBuffer direct) throws IOException { nativeRegister(direct); }
 
     private static native long nativeCreate(long poly, int window, int minLen, int maxLen,
-                                            int chunkLength, int algo, int device) throws IOException;
+                                            int chunkLength, int algo, int device, int predKind,
+                                            long predA, long predB) throws IOException;
     private static native void nativeDestroy(long h);
     private static native int nativeSlotCap(long h, int len);
     private static native int nativeDigestLen(long h);

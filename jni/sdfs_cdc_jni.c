@@ -105,11 +105,23 @@ static void throw_java(JNIEnv* env, const char* cls, const char* msg) {
     if (c) (*env)->ThrowNew(env, c, msg && *msg ? msg : "sdfs_cdc error");
 }
 
+/* predKind/predA/predB: the boundary detector's form (sdfs_cdc_params.pred_kind): SDFS_CDC_PRED_MASK
+ * -> (fp & predA) == predB, SDFS_CDC_PRED_DIV -> fp % predA == predB (the Java class reads them
+ * from the "sdfs.hip.boundary" system property; the default is the bitmask 0xFFF / 0). */
 JNIEXPORT jlong JNICALL CLS(nativeCreate)(JNIEnv* env, jclass cls, jlong poly, jint window, jint minLen,
-                                          jint maxLen, jint chunkLength, jint algo, jint device) {
+                                          jint maxLen, jint chunkLength, jint algo, jint device, jint predKind,
+                                          jlong predA, jlong predB) {
     (void)cls;
     sdfs_cdc_params p;
     sdfs_cdc_params_default(&p, 0);
+    p.pred_kind = (uint32_t)predKind;
+    if (predKind == SDFS_CDC_PRED_DIV) {
+        p.pred_div = (uint64_t)predA;
+        p.pred_rem = (uint64_t)predB;
+    } else {
+        p.pred_mask = (uint64_t)predA;
+        p.pred_value = (uint64_t)predB;
+    }
     p.poly = (uint64_t)poly;
     p.window = (uint32_t)window;
     p.min_len = (uint32_t)minLen;

@@ -46,7 +46,6 @@ static long chunk_ctx(const fast_ctx* c, const cdc_ref_params* p, const uint8_t*
                       uint32_t* lens, uint8_t* digests, size_t cap) {
     const size_t dl = cdc_ref_digest_len(p->hash_algo);
     const size_t W = p->window;
-    const uint64_t mask = p->pred_mask, val = p->pred_value;
     const size_t first = p->min_cmp == CDC_REF_MIN_GE ? (p->min_len ? p->min_len - 1 : 0) : p->min_len;
     uint64_t fp = 0;
     long count = 0;
@@ -62,7 +61,7 @@ static long chunk_ctx(const fast_ctx* c, const cdc_ref_params* p, const uint8_t*
         for (; k < len; k++) {
             fp = ((fp << 8) | buf[k]) ^ c->push[(fp >> c->shift) & 0xFF];
             if (k >= W) fp ^= c->pop[buf[k - W]];
-            if (k >= lo && (fp & mask) == val) {
+            if (k >= lo && cdc_ref_is_boundary(p, fp)) {
                 cut = k;
                 break;
             }

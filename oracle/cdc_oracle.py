@@ -32,6 +32,7 @@ FAST_LIB_PATH = os.path.join(HERE, "libcdc_fast.so")  # cdc_fast.c: bench.py's C
 
 SHA256, SHA256_160, MD5 = 0, 1, 2
 MIN_GT, MIN_GE = 0, 1
+PRED_MASK, PRED_DIV = 0, 1  # bitmask / divisor boundary detector
 DIGEST_LEN = {SHA256: 32, SHA256_160: 20, MD5: 16}
 
 POLY = 10923124345206883  # VariableSha256HashEngine.java:41, StorageServiceImpl.java:406
@@ -48,7 +49,9 @@ class CdcRefParams(ctypes.Structure):
         ("pred_mask", ctypes.c_uint64),
         ("pred_value", ctypes.c_uint64),
         ("hash_algo", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("pred_kind", ctypes.c_uint32),
+        ("pred_div", ctypes.c_uint64),
+        ("pred_rem", ctypes.c_uint64),
     ]
 
 
@@ -64,10 +67,24 @@ class Params:
     pred_mask: int = 0xFFF
     pred_value: int = 0
     hash_algo: int = SHA256
+    pred_kind: int = PRED_MASK  # PRED_DIV: fp % pred_div == pred_rem instead of the bitmask form
+    pred_div: int = 0
+    pred_rem: int = 0
 
     def to_c(self) -> CdcRefParams:
         return CdcRefParams(self.poly, self.window, self.min_len, self.max_len, self.min_cmp,
-                            self.pred_mask, self.pred_value, self.hash_algo, 0)
+                            self.pred_mask, self.pred_value, self.hash_algo, self.pred_kind,
+                            self.pred_div, self.pred_rem)
+
+    def is_boundary(self, fp):
+        """The boundary predicate on one fingerprint (int) or an array of them."""
+        if self.pred_kind == PRED_DIV:
+            if isinstance(fp, np.ndarray):
+                return (fp % np.uint64(self.pred_div)) == np.uint64(self.pred_rem)
+            return fp % self.pred_div == self.pred_rem
+        if isinstance(fp, np.ndarray):
+            return (fp & np.uint64(self.pred_mask)) == np.uint64(self.pred_value)
+        return (fp & self.pred_mask) == self.pred_value
 
     @property
     def digest_len(self) -> int:
@@ -325,7 +342,7 @@ def py_chunk(data: bytes, p: Params | None = None):
             fp ^= pop[ring.pop(0)]
         n += 1
         min_ok = n >= p.min_len if p.min_cmp == MIN_GE else n > p.min_len
-        if (min_ok and (fp & p.pred_mask) == p.pred_value) or n >= p.max_len:
+        if (min_ok and p.is_boundary(fp)) or n >= p.max_len:
             out.append((start, n, h(data[start: start + n])))
             start, n = k + 1, 0
     if n > 0:

@@ -254,7 +254,7 @@ long cdc_ref_chunk(const cdc_ref_params* p, const uint8_t* buf, size_t len, uint
         rabin_push(&r, buf[k]);
         n++;
         const int min_ok = (p->min_cmp == CDC_REF_MIN_GE) ? (n >= p->min_len) : (n > p->min_len);
-        const int boundary = (r.fp & p->pred_mask) == p->pred_value;
+        const int boundary = cdc_ref_is_boundary(p, r.fp);
         if ((min_ok && boundary) || n >= p->max_len) {
             if ((size_t)count >= cap) { rabin_free(&r); return -1; }
             starts[count] = (uint32_t)start;

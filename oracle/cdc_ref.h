@@ -33,6 +33,7 @@ extern "C" {
 
 enum { CDC_REF_SHA256 = 0, CDC_REF_SHA256_160 = 1, CDC_REF_MD5 = 2 };
 enum { CDC_REF_MIN_GT = 0, CDC_REF_MIN_GE = 1 };
+enum { CDC_REF_PRED_MASK = 0, CDC_REF_PRED_DIV = 1 };
 
 typedef struct cdc_ref_params {
     uint64_t poly;       /* Polynomial.createFromLong(10923124345206883L): bit i = coeff of x^i */
@@ -43,8 +44,18 @@ typedef struct cdc_ref_params {
     uint64_t pred_mask;  /* boundary predicate: (fp & mask) == value  (default 0xFFF, 0) */
     uint64_t pred_value;
     uint32_t hash_algo;  /* CDC_REF_SHA256 / _SHA256_160 / _MD5 */
-    uint32_t reserved;
+    uint32_t pred_kind;  /* CDC_REF_PRED_MASK: (fp & pred_mask) == pred_value (default);
+                            CDC_REF_PRED_DIV: fp % pred_div == pred_rem (SURVEY.md A.3's other
+                            candidate form of BoundaryDetectors.DEFAULT_BOUNDARY_DETECTOR) */
+    uint64_t pred_div;   /* divisor D >= 1 (CDC_REF_PRED_DIV) */
+    uint64_t pred_rem;   /* target remainder R (Java long %: fp >= 0, so R >= D never matches) */
 } cdc_ref_params;
+
+/* The boundary predicate on one window fingerprint. */
+static inline int cdc_ref_is_boundary(const cdc_ref_params* p, uint64_t fp) {
+    return p->pred_kind == CDC_REF_PRED_DIV ? (p->pred_div != 0 && fp % p->pred_div == p->pred_rem)
+                                            : (fp & p->pred_mask) == p->pred_value;
+}
 
 void cdc_ref_default_params(cdc_ref_params* p);
 int cdc_ref_poly_degree(uint64_t poly);

@@ -24,6 +24,7 @@ OK, EINVAL, ECAP, EHIP, ENOMEM, ENODEV = 0, -1, -2, -3, -4, -5
 FLAG_DIRECT = 1  # SDFS_CDC_FLAG_DIRECT: no coalescing of concurrent getChunks/getHash calls
 SHA256, SHA256_160, MD5 = 0, 1, 2
 MIN_GT, MIN_GE = 0, 1
+PRED_MASK, PRED_DIV = 0, 1  # sdfs_cdc_params.pred_kind: (fp & mask) == value / fp % div == rem
 RECORD_BYTES = 48
 NO_STREAM = (1 << 64) - 1  # SDFS_CDC_NO_STREAM
 ALL_DEVICES = -1           # sdfs_cdc_params.device: every gfx950 device
@@ -53,6 +54,10 @@ class Params(ctypes.Structure):
         ("flags", ctypes.c_uint32),
         ("max_batch_bytes", ctypes.c_uint64),
         ("device_mask", ctypes.c_uint64),
+        ("pred_kind", ctypes.c_uint32),  # ABI 3: boundary detector form
+        ("reserved2", ctypes.c_uint32),
+        ("pred_div", ctypes.c_uint64),
+        ("pred_rem", ctypes.c_uint64),
     ]
 
 

@@ -172,9 +172,21 @@ __device__ __forceinline__ void push_step(uint32_t& lo, uint32_t& hi, uint32_t d
 // Predicate kinds PK: 0 = (lo & mask) == val on one word, 1 = both words, 2 (mirrored state
 // only) = the low k fp bits all zero, i.e. `lo` (here the mirrored hi word) < a.thr = 2^(32-k).
 // `lo` is the word holding fp bits 0..31 (mirrored: R's hi word, masks bit-reversed by the host).
+// PK 3 (mirrored state only) is the divisor detector fp % D == R: fp = bitrev64(R) < 2^53 is exact
+// in f64, q = floor(fp * (1/D)) is within one of floor(fp / D) (for D >= 3 — the host runs powers
+// of two as masks — the two roundings leave an absolute error <= fp/D * 2^-52 < 2^53/3 * 2^-52 < 1),
+// so r = fp - q*D (one exact fma) is the remainder t or t -/+ D, and exactly one of r, r + D, r - D
+// lies in [0, D): the test is true iff t == R (the host passes R >= D as NaN: never true).
 template <int PK>
 __device__ __forceinline__ void cand_shift(uint32_t& bits, uint32_t lo, uint32_t hi, const ScanArgs& a) {
-    if constexpr (PK == 2) {
+    if constexpr (PK == 3) {
+        const uint32_t flo = __builtin_bitreverse32(lo), fhi = __builtin_bitreverse32(hi);
+        const double f = __builtin_fma((double)fhi, 4294967296.0, (double)flo);
+        const double q = __builtin_floor(f * a.div_inv);
+        const double r = __builtin_fma(-q, a.div_d, f);
+        const uint32_t h = (r == a.rem_d) | (r + a.div_d == a.rem_d) | (r - a.div_d == a.rem_d);
+        asm("v_lshl_or_b32 %0, %0, 1, %1" : "+v"(bits) : "v"(h));
+    } else if constexpr (PK == 2) {
         asm("v_cmp_gt_u32 vcc, %2, %1\n\t"
             "v_addc_co_u32 %0, vcc, %0, %0, vcc"
             : "+v"(bits)
@@ -1191,7 +1203,7 @@ __device__ __forceinline__ void scan_iter(const ScanArgs& a, const uint8_t* tab,
 template <int W, int PK, class CFG>
 __global__ __launch_bounds__(CFG::kThreads, CFG::kWavesPerSimd) void cdc_scan_kernel(ScanArgs a) {
     static_assert(!CFG::kMirror || !CFG::kPrefetch, "mirrored state: no prefetch");
-    static_assert(CFG::kMirror || PK != 2, "the one-compare predicate needs the mirrored state");
+    static_assert(CFG::kMirror || PK < 2, "the one-compare and divisor predicates need the mirrored state");
     constexpr int NCH = CFG::kChains;
     constexpr int C = CFG::kCopies;
     __shared__ __attribute__((aligned(16))) uint8_t tab[CFG::kLds];

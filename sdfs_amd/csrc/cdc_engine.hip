@@ -267,6 +267,7 @@ struct DevEngine {
     int fused_probe = 0;  // form (cdc_sweep_r3.hip launch_fused_probe)
     hipEvent_t ev_front = nullptr;
     ScanVariantInfo scan_info{};
+    bool pred_div = false;  // divisor detector evaluated as such (scan predicate kind 3)
     uint32_t first_off = 0;
     uint32_t bin_shift = 0, nbins = 1;
     uint32_t digest_len = 32;
@@ -323,7 +324,16 @@ int validate(const sdfs_cdc_params* p) {
     if (p->max_len == 0) return fail(SDFS_CDC_EINVAL, "max_len must be > 0");
     if (p->min_cmp > SDFS_CDC_MIN_GE) return fail(SDFS_CDC_EINVAL, "bad min_cmp");
     if (p->hash_algo > SDFS_CDC_MD5) return fail(SDFS_CDC_EINVAL, "bad hash_algo");
-    if (p->pred_mask >> d) return fail(SDFS_CDC_EINVAL, "pred_mask has bits above the fp degree");
+    if (p->pred_kind > SDFS_CDC_PRED_DIV) return fail(SDFS_CDC_EINVAL, "bad pred_kind %u", p->pred_kind);
+    if (p->pred_kind == SDFS_CDC_PRED_MASK && (p->pred_mask >> d))
+        return fail(SDFS_CDC_EINVAL, "pred_mask has bits above the fp degree");
+    if (p->pred_kind == SDFS_CDC_PRED_DIV) {
+        if (p->pred_div == 0 || (p->pred_div >> 32))
+            return fail(SDFS_CDC_EINVAL, "pred_div must be in [1, 2^32)");
+        // a divisor other than a power of two is evaluated in f64: the window fp must be exact
+        if ((p->pred_div & (p->pred_div - 1)) != 0 && d > 53)
+            return fail(SDFS_CDC_EINVAL, "divisor predicate needs a polynomial of degree <= 53 (got %d)", d);
+    }
     if (p->flags & ~(uint32_t)SDFS_CDC_FLAG_DIRECT) return fail(SDFS_CDC_EINVAL, "unknown flags 0x%x", p->flags);
     if (p->device < -1 && !p->device_mask) return fail(SDFS_CDC_EINVAL, "device %d (-1 = every gfx950 device)", p->device);
     return SDFS_CDC_OK;
@@ -482,7 +492,14 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
         sa.mask_hi = bitrev32_host((uint32_t)(m >> 32));
         sa.val_lo = bitrev32_host((uint32_t)v);
         sa.val_hi = bitrev32_host((uint32_t)(v >> 32));
-        if (!pred64 && m != 0 && (m & (m + 1)) == 0 && v == 0) {  // low k bits zero: one compare
+        if (e->pred_div) {
+            // divisor detector: fp % D == R in f64 (cdc_device.h cand_shift<3>); R >= D never
+            // matches, which a NaN target expresses (no comparison with NaN holds)
+            pk = 3;
+            sa.div_d = (double)e->prm.pred_div;
+            sa.div_inv = 1.0 / sa.div_d;
+            sa.rem_d = e->prm.pred_rem < e->prm.pred_div ? (double)e->prm.pred_rem : __builtin_nan("");
+        } else if (!pred64 && m != 0 && (m & (m + 1)) == 0 && v == 0) {  // low k bits zero: one compare
             const int k = __builtin_popcountll(m);
             sa.thr = k == 32 ? 1u : 1u << (32 - k);
             pk = 2;
@@ -1190,6 +1207,17 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     e->prm = *p;
     e->prm.device = ordinal;
     e->degree = poly_degree(p->poly);
+    if (p->pred_kind == SDFS_CDC_PRED_DIV) {
+        // fp >= 0, so fp % 2^k == R < 2^k is the bitmask detector (fp & (2^k - 1)) == R: run the
+        // mask kernels for it; any other divisor (or R >= D, never true) takes the f64 form
+        const uint64_t dv = p->pred_div;
+        if ((dv & (dv - 1)) == 0 && p->pred_rem < dv) {
+            e->prm.pred_mask = dv - 1;
+            e->prm.pred_value = p->pred_rem;
+        } else {
+            e->pred_div = true;
+        }
+    }
     e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     e->first_off = p->min_cmp == SDFS_CDC_MIN_GT ? p->min_len : (p->min_len ? p->min_len - 1 : 0);
     e->digest_len = p->hash_algo == SDFS_CDC_SHA256 ? 32 : (p->hash_algo == SDFS_CDC_SHA256_160 ? 20 : 16);
@@ -1242,6 +1270,8 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     e->scan_info = scan_variant_info(e->scan_variant);
     if (e->scan_info.copies == 0 || e->seg_len == 0 || (e->seg_len % e->scan_info.blk) != 0)
         return fail(SDFS_CDC_EINVAL, "bad scan variant/segment length");
+    if (e->pred_div && (e->scan_variant != 0 || !e->scan_info.mirror))
+        return fail(SDFS_CDC_EINVAL, "the divisor predicate runs on the production scan only");
     std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies, e->scan_info.mirror != 0,
                                                  e->scan_info.pop_swap != 0);
     if (e->zero_page.ensure(256) != hipSuccess || hipMemset(e->zero_page.p, 0, 256) != hipSuccess ||
@@ -1507,11 +1537,12 @@ int device_set(const sdfs_cdc_params* p, std::vector<int>* ords) {
 // Engines are shared between handles whose parameters (other than the device fields) and device
 // sets are equal.
 std::string share_key(const sdfs_cdc_params* p, const std::vector<int>& ords) {
-    char buf[256];
-    snprintf(buf, sizeof(buf), "%llx/%u/%u/%u/%u/%llx/%llx/%u/%u/%x/%llx|",
+    char buf[384];
+    snprintf(buf, sizeof(buf), "%llx/%u/%u/%u/%u/%llx/%llx/%u/%u/%x/%llx/%u/%llx/%llx|",
              (unsigned long long)p->poly, p->window, p->min_len, p->max_len, p->chunk_length,
              (unsigned long long)p->pred_mask, (unsigned long long)p->pred_value, p->min_cmp, p->hash_algo, p->flags,
-             (unsigned long long)p->max_batch_bytes);
+             (unsigned long long)p->max_batch_bytes, p->pred_kind, (unsigned long long)p->pred_div,
+             (unsigned long long)p->pred_rem);
     std::string k(buf);
     for (int o : ords) k += std::to_string(o) + ",";
 #ifdef SDFS_TUNING
@@ -1608,8 +1639,20 @@ struct Coll {
 
 // One all-gather per device of the set inside one RCCL group.  ncclGroupEnd runs on every path
 // once ncclGroupStart succeeded, so a failing device never leaves the group open on this thread.
+// Every device is selected once BEFORE the group opens: a hipSetDevice failure is not an RCCL
+// error, so inside the group it would let ncclGroupEnd launch the all-gathers of the devices
+// before it, whose kernels would then wait for peers that were never enqueued.  Failures RCCL
+// itself reports (an ncclAllGather that fails inside the group) are the group's to abort.
 template <class Issue>
 int grouped_all_gather(const RcclApi* api, Set& s, Issue&& issue) {
+    for (int i = 0; i < (int)s.ndev(); i++) {
+        const hipError_t he = hipSetDevice(s.ordinals[i]);
+        if (he != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(SDFS_CDC_EHIP, "hipSetDevice(%d) failed before the all-gather group: %s", s.ordinals[i],
+                        hipGetErrorString(he));
+        }
+    }
     const int g = api->group_start();
     if (g) return fail(SDFS_CDC_EHIP, "ncclGroupStart failed: %s", api->errstr(g));
     int rc = SDFS_CDC_OK;

@@ -76,7 +76,7 @@ constexpr uint32_t kSegSumWords = 8;  // summary u16 x 8 (4 words) | ncand | ovf
 constexpr uint32_t kJoinExtra = 8;  // true chunk starts a section may take before its chains meet
 constexpr uint32_t kJoinWords = 2 + kJoinExtra;
 // Section length of the sectioned cut walk for a buffer of `len` bytes (0 = not sectioned).
-uint32_t resolve_section_len(uint64_t len, uint32_t max_len, uint32_t sec_log2 = 20);
+uint32_t resolve_section_len(uint64_t len, uint32_t max_len, uint32_t sec_log2 = 18);
 
 struct ScanArgs {
     const uint8_t* data;
@@ -92,6 +92,7 @@ struct ScanArgs {
                                  // (hi word), mirrored 64 - deg(P) (lo word of bitrev64(fp))
     uint32_t mask_lo, mask_hi, val_lo, val_hi;  // mirrored: bit-reversed, lo = the word of fp bits 0..31
     uint32_t thr;                // predicate kind 2: 2^(32-k) for a zero test of the low k fp bits
+    double div_d, div_inv, rem_d;  // predicate kind 3 (divisor detector): D, 1/D, R as f64 (fp < 2^53)
     const uint8_t* tab_image;    // global copy of the LDS image (scan_lds_bytes(copies))
     const uint8_t* zero_page;    // 256 zero bytes (branch-free prefetch of tail blocks)
     // fused cut resolution: when every wave's 64 segments are exactly one buffer (uniform layout,
@@ -195,7 +196,7 @@ inline uint64_t splitmix64_host(uint64_t x) {
 hipError_t launch_seg_prefix(const uint32_t* lens, uint32_t nbuf, uint32_t seg_len, uint64_t* seg_prefix,
                              hipStream_t stream);
 // pk: predicate kind (cand_shift): 0 = one 32-bit word, 1 = both words, 2 = low-k zero (mirrored
-// variants only)
+// variants only), 3 = divisor detector fp % D == R (production variant only)
 hipError_t launch_scan(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
                        hipStream_t stream);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);

@@ -66,10 +66,13 @@ bool scan_window_supported(int window) {
 
 template <int W, class CFG>
 static hipError_t launch_scan_wc(const ScanArgs& a, int pk, int grid, int block, hipStream_t s) {
+    static_assert(CFG::kMirror, "the production scan rolls the mirrored state");
     if (pk == 1)
         hipLaunchKernelGGL((cdc_scan_kernel<W, 1, CFG>), dim3(grid), dim3(block), 0, s, a);
-    else if (pk == 2 && CFG::kMirror)
-        hipLaunchKernelGGL((cdc_scan_kernel<W, CFG::kMirror ? 2 : 0, CFG>), dim3(grid), dim3(block), 0, s, a);
+    else if (pk == 2)
+        hipLaunchKernelGGL((cdc_scan_kernel<W, 2, CFG>), dim3(grid), dim3(block), 0, s, a);
+    else if (pk == 3)
+        hipLaunchKernelGGL((cdc_scan_kernel<W, 3, CFG>), dim3(grid), dim3(block), 0, s, a);
     else
         hipLaunchKernelGGL((cdc_scan_kernel<W, 0, CFG>), dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();
@@ -445,7 +448,15 @@ __global__ __launch_bounds__(256) void cdc_resolve_place_kernel(ResolveArgs a) {
         const uint32_t b = item / a.nsec, j = item - b * a.nsec;
         const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
         const uint32_t nsb = (len + a.sec_len - 1) / a.sec_len;  // sections of this buffer
-        if (j >= nsb) continue;
+        if (j >= nsb) {
+            // an empty buffer (nsb = 0) has no section of its own: its first item settles it here,
+            // so the stitch kernel skips it and no stale flag or count of an earlier batch survives
+            if (nsb == 0 && j == 0 && lane == 0) {
+                a.join_bad[b] = 0u;
+                a.counts[b] = 0u;
+            }
+            continue;
+        }
         const uint32_t* jb = a.join + (uint64_t)b * a.nsec * kJoinWords;
         const uint32_t* cb = a.spec_cnt + (uint64_t)b * a.nsec;
         // every section joined?  chunks before this section, and in the whole buffer
@@ -591,11 +602,11 @@ __global__ __launch_bounds__(256) void cdc_resolve_stitch_kernel(ResolveArgs a) 
 
 uint32_t resolve_section_len(uint64_t len, uint32_t max_len, uint32_t sec_log2) {
     // sections of 2^sec_log2 positions for buffers of 4 MiB and more (40 MiB backup buffers at the
-    // default 1 Mi: 40 sections); a section must hold a chunk of max_len
-    const uint64_t sec = 1ull << sec_log2;
-    if (len < (4ull << 20) || len >= (1ull << 31) || (uint64_t)max_len + 64 >= 32ull * kResStride ||
-        sec < 2ull * max_len)
-        return 0;
+    // engine's default 2^18: 160 sections); a section must hold two chunks of max_len, so a larger
+    // max_len grows the section to the next power of two instead of giving up the sectioned walk
+    if (len < (4ull << 20) || len >= (1ull << 31) || (uint64_t)max_len + 64 >= 32ull * kResStride) return 0;
+    uint64_t sec = 1ull << sec_log2;
+    while (sec < 2ull * max_len) sec <<= 1;
     return (uint32_t)sec;
 }
 

@@ -98,3 +98,75 @@ class DeviceBatch:
         """Dense fingerprint table (total x 48 B) as a device tensor view."""
         n = int(self.total.item())
         return self.recs[: n * _lib.RECORD_BYTES].view(n, _lib.RECORD_BYTES)
+
+    def fill_tar(self, layout: "TarLayout") -> None:
+        """Write the tar-like stream of ``layout`` into the batch, piece by piece, with the engine's
+        device generator (zero padding by memset); the batch holds stream bytes [0, nbytes)."""
+        if layout.total != self.nbytes:
+            raise ValueError(f"layout covers {layout.total} bytes, the batch holds {self.nbytes}")
+        st = self.torch.cuda.current_stream().cuda_stream
+        base = self.data.data_ptr()
+        for dst, n, src in layout.pieces:
+            if src < 0:
+                self.data[dst:dst + n].zero_()
+            else:
+                self.engine.synth_device(base + dst, n, layout.seed, src, 0, stream=st)
+
+
+# ---- BASELINE.json configs[4]: the BACKUP_VOLUME archive profile's tar-like stream ----
+TAR_SEED = 0x7A5_5DF5
+TAR_HEADER_STREAM = 1 << 40  # header of file k = synthetic stream TAR_HEADER_STREAM + k
+TAR_BODY_STREAM = 1 << 41    # fresh body of file k = synthetic stream TAR_BODY_STREAM + k
+
+
+@dataclass
+class TarLayout:
+    """A tar-like sequential stream ("512-B headers + PRNG file bodies whose
+    lengths are log-uniform 1 KiB-64 MiB; 20 % of bodies repeat an earlier body"), as the
+    BACKUP_VOLUME profile (VolumeConfigWriter.java:298-307) would receive it from a backup tool.
+    Like ustar, every member is a 512-byte header followed by its body zero-padded to a multiple of
+    512.  ``pieces`` = (stream offset, length, source stream or -1 for zeros) covering [0, total)
+    in order (a source piece is bytes [0, length) of that counter-based synthetic stream);
+    ``repeats`` = (copy offset, original offset, length) of every repeated body."""
+
+    total: int
+    seed: int
+    pieces: list
+    bodies: list   # (stream offset, length, source stream) of every body
+    repeats: list
+
+
+def tar_layout(total: int, seed: int = TAR_SEED, repeat_p: float = 0.2, lo_log2: float = 10.0,
+               hi_log2: float = 26.0) -> TarLayout:
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    pieces, bodies, repeats = [], [], []
+    fresh = []  # indices into bodies of non-repeated bodies
+    p = k = 0
+    while p < total:
+        h = min(512, total - p)
+        pieces.append((p, h, TAR_HEADER_STREAM + k))
+        p += h
+        if p >= total:
+            break
+        n = int(2.0 ** rng.uniform(lo_log2, hi_log2))
+        src = TAR_BODY_STREAM + k
+        orig = None
+        if fresh and rng.random() < repeat_p:
+            orig = bodies[fresh[int(rng.integers(0, len(fresh)))]]
+            n, src = orig[1], orig[2]  # the whole earlier body, byte for byte
+        n = min(n, total - p)
+        pieces.append((p, n, src))
+        if orig is not None:
+            repeats.append((p, orig[0], n))
+        else:
+            fresh.append(len(bodies))
+        bodies.append((p, n, src))
+        p += n
+        pad = min((-n) % 512, total - p)
+        if pad:
+            pieces.append((p, pad, -1))
+            p += pad
+        k += 1
+    return TarLayout(total, seed, pieces, bodies, repeats)

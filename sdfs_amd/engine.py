@@ -63,7 +63,9 @@ class SdfsConfig:
     ``window``        variable-window-size (Config.java:160-161; 48)
     ``hash_type``     hash-type (Config.java:150-151; VARIABLE_SHA256, VolumeConfigWriter.java:109)
     The boundary-predicate knobs are not SDFS settings (the jar's detector is static,
-    SURVEY.md A.1); they are exposed because the jar is absent and they are unpinned (A.3).
+    SURVEY.md A.1); they are exposed because the jar is absent and they are unpinned (A.3):
+    ``pred_kind`` PRED_MASK -> ``(fp & pred_mask) == pred_value``, PRED_DIV -> ``fp % pred_div ==
+    pred_rem`` (the two detector forms A.3 names).
     """
 
     chunk_length: int = 256 * 1024
@@ -74,6 +76,9 @@ class SdfsConfig:
     poly: int = POLY
     pred_mask: int = 0xFFF
     pred_value: int = 0
+    pred_kind: int = _lib.PRED_MASK  # PRED_DIV: the divisor detector fp % pred_div == pred_rem
+    pred_div: int = 0
+    pred_rem: int = 0
     min_cmp: int = MIN_GT
     max_batch_bytes: int = 0  # host-batch pinned staging per slot (0 = the engine default, 256 MiB)
     direct: bool = False      # SDFS_CDC_FLAG_DIRECT: one GPU round trip per call (no coalescing)
@@ -131,6 +136,9 @@ class SdfsConfig:
         p.chunk_length = self.chunk_length
         p.pred_mask = self.pred_mask
         p.pred_value = self.pred_value
+        p.pred_kind = self.pred_kind
+        p.pred_div = self.pred_div
+        p.pred_rem = self.pred_rem
         p.min_cmp = self.min_cmp
         p.max_batch_bytes = self.max_batch_bytes
         p.flags = _lib.FLAG_DIRECT if self.direct else 0

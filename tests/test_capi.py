@@ -50,11 +50,12 @@ def test_python_binding_covers_header():
 
 
 def test_struct_layouts_match_header():
-    # sdfs_cdc_params: 8+4+4+4+4+8+8+4+4+4+4+8+8 = 72 bytes (ABI 2 added device_mask);
-    # sdfs_cdc_dev_out: 4 ptrs + 2 u32 + ptr + u64 + ptr
-    assert ctypes.sizeof(_lib.Params) == 72
+    # sdfs_cdc_params: 8+4+4+4+4+8+8+4+4+4+4+8+8 = 72 bytes (ABI 2 added device_mask), + 4+4+8+8
+    # (ABI 3: pred_kind, reserved2, pred_div, pred_rem) = 96; sdfs_cdc_dev_out: 4 ptrs + 2 u32 +
+    # ptr + u64 + ptr
+    assert ctypes.sizeof(_lib.Params) == 96
     assert ctypes.sizeof(_lib.DevOut) == 64
-    assert _lib.load().sdfs_cdc_abi_version() == 2
+    assert _lib.load().sdfs_cdc_abi_version() == 3
 
 
 def test_default_params_are_the_reference_defaults():

@@ -30,7 +30,9 @@ def engine_for(prm: dict):
     key = tuple(sorted(prm.items()))
     if key not in _ENGINES:
         cfg = SdfsConfig(min_len=prm["min_len"], max_len=prm["max_len"], window=prm["window"], poly=prm["poly"],
-                         pred_mask=prm["pred_mask"], pred_value=prm["pred_value"], min_cmp=prm["min_cmp"])
+                         pred_mask=prm["pred_mask"], pred_value=prm["pred_value"], min_cmp=prm["min_cmp"],
+                         pred_kind=prm.get("pred_kind", 0), pred_div=prm.get("pred_div", 0),
+                         pred_rem=prm.get("pred_rem", 0))
         algo = prm["hash_algo"]
         if algo == O.MD5:
             e = HipVariableMD5HashEngine(cfg)
@@ -582,6 +584,71 @@ def test_config4_backup_per_gpu_share_16gib():
     assert 7000 < mean < 9000, mean
 
 
+def test_config4_tar_stream_per_gpu_share_16gib():
+    """BASELINE configs[4] (BACKUP_VOLUME, 128 GiB tar-like stream over 8 GPUs) at one GPU's share
+    with its real content: 409 write buffers of 40 MiB = 16 GiB of 512-byte headers, log-uniform
+    1 KiB-64 MiB bodies zero-padded to 512 and 20 % repeated bodies (sdfs_amd.device.tar_layout,
+    SURVEY.md 8(d) B4), maxLen 128 KiB (VolumeConfigWriter.java:298-307).  Exact cover / min / max on
+    every buffer; the first and last buffers and the buffers holding repeated bodies and their
+    originals equal the oracle; and a repeated body dedups: after the first cut inside it, its
+    chunks are the original's chunks (same offsets in the body, same digests)."""
+    from sdfs_amd.device import tar_layout
+
+    prm = P(max_len=131072)
+    e = engine_for(prm)
+    nbuf, L = 409, 40960 * 1024
+    lay = tar_layout(nbuf * L)
+    assert len(lay.repeats) > 50 and len(lay.bodies) > 500
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=L, records=False)
+    batch.fill_tar(lay)
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    _check_cover(counts, st, ln, L, prm)
+    mean = nbuf * L / total
+    assert 6000 < mean < 9000, mean
+    # repeated bodies of >= 4 MiB: chunk lists realign
+    valid = np.arange(st.shape[1])[None, :] < counts[:, None]
+    gs = (st.astype(np.int64) + (np.arange(nbuf, dtype=np.int64) * L)[:, None])[valid]
+    gl = ln.astype(np.int64)[valid]
+    gd = dg[valid]
+    order = np.argsort(gs)
+    gs, gl, gd = gs[order], gl[order], gd[order]
+
+    def inside(a, n):
+        i0, i1 = np.searchsorted(gs, a), np.searchsorted(gs, a + n)
+        keep = [i for i in range(i0, i1) if gs[i] + gl[i] <= a + n]
+        return {(int(gs[i] - a), int(gl[i])): bytes(gd[i]) for i in keep}
+
+    checked = 0
+    sample = {0, nbuf - 1}
+    for c, o, n in lay.repeats:
+        if n < (4 << 20):
+            continue
+        cp, og = inside(c, n), inside(o, n)
+        common = set(cp) & set(og)
+        assert all(cp[k] == og[k] for k in common)
+        covered = sum(k[1] for k in common) / max(sum(k[1] for k in cp), 1)
+        assert covered > 0.9, (c, o, n, covered)
+        if checked < 3:
+            sample |= {c // L, o // L}
+        checked += 1
+    assert checked >= 10
+    # sampled buffers against the oracle
+    sample = sorted(sample)
+    host = np.stack([G.tar_bytes(lay, b * L, L) for b in sample])
+    dev = batch.data.view(nbuf, L)
+    for j, b in enumerate(sample):
+        assert torch.equal(dev[b].cpu(), torch.from_numpy(host[j])), b
+    offs = (np.arange(len(sample), dtype=np.uint64) * L).astype(np.uint64)
+    ec, es, el, ed = O.chunk_batch(host.reshape(-1), offs, np.full(len(sample), L, np.uint32), O.Params(**prm),
+                                   nthreads=16)
+    for j, b in enumerate(sample):
+        c = int(ec[j])
+        assert counts[b] == c and (st[b, :c] == es[j, :c]).all() and (ln[b, :c] == el[j, :c]).all(), b
+        assert (dg[b, :c] == ed[j, :c]).all(), b
+
+
 _SCAN_VARIANT_CHECK = r"""
 import os, sys
 import numpy as np
@@ -805,3 +872,61 @@ def test_fused_list_walk_edges(prm):
         assert c == len(es), b
         assert st[b, :c].tolist() == es.tolist() and ln[b, :c].tolist() == el.tolist(), b
         assert (dg[b, :c, :dl] == ed).all(), b
+
+
+def test_sectioned_batch_with_empty_buffers_after_a_full_batch():
+    """A ragged host batch holding a >= 4 MiB buffer (sectioned walk with the parallel join/place)
+    and EMPTY buffers, run right after batches that left non-zero counts in the reused result
+    slots: an empty buffer has no section, so the place kernel settles it (count 0) — before, its
+    join flag was stale workspace memory and a stale count could come back."""
+    prm = P()
+    e = engine_for(prm)
+    for _ in range(2):
+        full = O.synth(SYNTH_SEED, 1400, 0, 4 * 262144)
+        c0, *_ = e.chunk_batch(full, np.arange(4, dtype=np.uint64) * 262144, np.full(4, 262144, np.uint32))
+        assert (c0 > 0).all()
+        lens = np.array([0, 5 * 2**20 + 3, 0, 300000, 0], dtype=np.uint32)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+        base = O.synth(SYNTH_SEED, 1401, 0, int(lens.sum()))
+        counts, st, ln, dg = e.chunk_batch(base, offs, lens)
+        for b in range(len(lens)):
+            if lens[b] == 0:
+                assert counts[b] == 0, b
+                continue
+            buf = base[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+            c = counts[b]
+            assert_same((st[b, :c], ln[b, :c], dg[b, :c]), O.chunk(buf, O.Params(**prm)), b)
+
+
+def test_piece_mode_sections_joined_and_stitched():
+    """Piece mode: a uniform batch of long buffers large enough for full 4 KiB scan segments
+    (>= num_cus * 4 * 64 of them) whose 256 Ki-position sections are exactly one wave's 64
+    segments, so the scan's epilogue walks every section from the lanes' summaries and the bitmap is
+    stored only sparsely.  Buffers whose sections never join (all zero; a zero run across sections;
+    cuts out of phase with the sections) take the stitch fallback, which then searches the segment
+    summaries (find_first_sum).  Every buffer against the oracle."""
+    prm = P(min_len=2999, max_len=131072)
+    L, nbuf = 5 * 2**20, 64
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    # the engine's piece-mode conditions (cdc_engine.hip run_pipeline): full-length segments for a
+    # batch of >= ncu*4*64 of them, section = 2^18 positions = 64 segments of 4 KiB, uniform_len % section == 0
+    assert nbuf * L // 4096 >= ncu * 4 * 64 and L % (1 << 18) == 0 and 2 * prm["max_len"] <= (1 << 18)
+    e = engine_for(prm)
+    batch = DeviceBatch(e, nbuf=nbuf, buf_len=L)
+    batch.fill_streams(first_stream=1500, bufs_per_stream=1)
+    v = batch.data.view(nbuf, L)
+    v[1].zero_()
+    v[4, 1_000_000:3_500_000].zero_()
+    v[9, 262_100:262_200].zero_()
+    v[17, :].fill_(0x5A)               # constant: no candidates, forced cuts only
+    v[33, 2**20:].zero_()
+    batch.run()
+    counts, st, ln, dg, total = batch.host_results()
+    assert total == int(counts.sum())
+    host = v.cpu().numpy()
+    offs = (np.arange(nbuf, dtype=np.uint64) * L).astype(np.uint64)
+    ec, es, el, ed = O.chunk_batch(host.reshape(-1), offs, np.full(nbuf, L, np.uint32), O.Params(**prm), nthreads=16)
+    for b in range(nbuf):
+        c = int(ec[b])
+        assert counts[b] == c and (st[b, :c] == es[b, :c]).all() and (ln[b, :c] == el[b, :c]).all(), b
+        assert (dg[b, :c] == ed[b, :c]).all(), b

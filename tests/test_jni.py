@@ -41,7 +41,7 @@ class Jni:
         f = getattr(g, PFX + "nativeCreate")
         f.restype = ctypes.c_int64
         f.argtypes = [VP, VP, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                      ctypes.c_int32, ctypes.c_int32]
+                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64]
         getattr(g, PFX + "nativeDestroy").argtypes = [VP, VP, ctypes.c_int64]
         for n in ("nativeSlotCap",):
             getattr(g, PFX + n).argtypes = [VP, VP, ctypes.c_int64, ctypes.c_int32]
@@ -87,7 +87,7 @@ def test_create_without_device_throws_ioexception():
     except ImportError:
         pass
     j = Jni()
-    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, 0, 0)
+    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, 0, 0, 0, 0xFFF, 0)
     assert h == 0
     cls, msg = j.exception()
     assert cls == "java/io/IOException" and msg
@@ -97,7 +97,7 @@ def test_create_without_device_throws_ioexception():
 @pytest.mark.parametrize("algo", [0, 1, 2])
 def test_jni_get_chunks_and_get_hash_vs_oracle(algo):
     j = Jni()
-    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, algo, 0)
+    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, algo, 0, 0, 0xFFF, 0)
     assert h and j.exception() is None
     dl = j.call("nativeDigestLen", h)
     assert dl == (32, 20, 16)[algo]
@@ -132,7 +132,7 @@ def test_jni_get_chunks_and_get_hash_vs_oracle(algo):
     from sdfs_amd import _lib
     lib = _lib.load()
     k = lib.sdfs_cdc_share_count(ctypes.c_void_p(h))  # (other live instances of this process count too)
-    h2 = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, algo, 0)
+    h2 = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, algo, 0, 0, 0xFFF, 0)
     assert h2 and h2 != h and j.exception() is None
     assert lib.sdfs_cdc_share_count(ctypes.c_void_p(h)) == k + 1 == lib.sdfs_cdc_share_count(ctypes.c_void_p(h2))
     j.call("nativeDestroy", h)
@@ -169,7 +169,7 @@ def test_fill_failure_is_einval_with_its_own_message():
     eng.destroy()
     # through the glue: the injected ArrayIndexOutOfBoundsException stays the pending exception
     j = Jni()
-    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, 0, 0)
+    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, 0, 0, 0, 0xFFF, 0)
     assert h and j.exception() is None
     arr = j.byte_array(data)
     c = j.call("nativeSlotCap", h, len(data))
@@ -182,4 +182,31 @@ def test_fill_failure_is_einval_with_its_own_message():
     assert j.call("nativeGetChunks", h, arr, -1, st, ln, dg) == len(es) and j.exception() is None
     for a in (arr, st, ln, dg):
         j.stub.stub_free(a)
+    j.call("nativeDestroy", h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,a,b", [(1, 4099, 0), (1, 8192, 8191), (0, 0x7FF, 0x15)])
+def test_jni_boundary_detector_forms_vs_oracle(kind, a, b):
+    """The Java class passes the detector form of "sdfs.hip.boundary" (mask:M:V / div:D:R) through
+    nativeCreate; every form chunks like the oracle with the same detector."""
+    j = Jni()
+    h = j.call("nativeCreate", O.POLY, 48, 4095, 32768, 262144, 0, 0, kind, a, b)
+    assert h and j.exception() is None
+    prm = (O.Params(pred_kind=O.PRED_DIV, pred_div=a, pred_rem=b) if kind == 1 else
+           O.Params(pred_mask=a, pred_value=b))
+    for n in (5000, 262144):
+        data = O.synth(O.SYNTH_SEED, 5100 + n % 89, 0, n).tobytes()
+        cap = j.call("nativeSlotCap", h, n)
+        arr = j.byte_array(data)
+        st, ln, dg = j.new(2, cap), j.new(2, cap), j.new(1, cap * 32)
+        cnt = j.call("nativeGetChunks", h, arr, -1, st, ln, dg)
+        assert j.exception() is None
+        es, el, ed = O.chunk(data, prm)
+        assert cnt == len(es)
+        assert j.read(st, np.int32, cnt).tolist() == es.tolist()
+        assert j.read(ln, np.int32, cnt).tolist() == el.tolist()
+        assert j.read(dg, np.uint8, cnt * 32).tobytes() == ed.tobytes()
+        for x in (arr, st, ln, dg):
+            j.stub.stub_free(x)
     j.call("nativeDestroy", h)

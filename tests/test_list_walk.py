@@ -78,7 +78,7 @@ def greedy(pos, n, p_):
 
 def candidates(data, p_):
     fp = O.window_fps(data, p_.poly, p_.window)
-    return np.flatnonzero((fp & np.uint64(p_.pred_mask)) == np.uint64(p_.pred_value)).astype(np.int64)
+    return np.flatnonzero(p_.is_boundary(fp)).astype(np.int64)
 
 
 @pytest.mark.parametrize("min_len,max_len,mask", [

@@ -91,7 +91,9 @@ def test_chunk_list_contract(fx):
 
 
 @pytest.mark.parametrize("name", ["rand_256k", "rand_256k_ge", "rand_256k_small", "rand_256k_dense", "hole_256k",
-                                  "zeros_256k", "rand_256k_mask64", "rand_256k_min0", "rand_256k_w64"])
+                                  "zeros_256k", "rand_256k_mask64", "rand_256k_min0", "rand_256k_w64",
+                                  "div4099_r0_256k", "div3_dense_256k", "div4099_never_256k", "div4099_zeros_256k",
+                                  "div8192_rmax_256k"])
 def test_two_phase_formulation_equals_rolling_loop(name):
     """The GPU computes a candidate bitmap over ALL positions, then resolves cuts greedily; that
     must equal the reference's byte-serial loop for every knob combination."""
@@ -99,7 +101,7 @@ def test_two_phase_formulation_equals_rolling_loop(name):
     data = G.fixture_input(fx)
     p = G.oracle_params(fx)
     fps = O.window_fps(data, p.poly, p.window)
-    cand = (fps & np.uint64(p.pred_mask)) == np.uint64(p.pred_value)
+    cand = p.is_boundary(fps)
     got = O.resolve_from_candidates(cand, len(data), p)
     assert got == list(zip(fx["starts"], fx["lens"]))
 
@@ -147,3 +149,25 @@ def test_fast_cpu_form_edge_lengths_and_params():
                 assert np.array_equal(x, y), (n, p)
     z = np.zeros(262144, np.uint8)
     assert np.array_equal(O.chunk_fast(z)[1], O.chunk(z)[1])
+
+
+def test_divisor_detector_power_of_two_is_the_mask_and_others_differ():
+    """fp >= 0, so fp % 2^k == R is (fp & (2^k-1)) == R (the engine runs it as the mask); a divisor
+    that is not a power of two picks other boundaries; C loop == Python loop for the divisor form."""
+    data = O.synth(O.SYNTH_SEED, 4321, 0, 200000).tobytes()
+    for k, r in ((12, 0), (12, 4095), (13, 77)):
+        a = O.chunk(data, O.Params(pred_kind=O.PRED_DIV, pred_div=1 << k, pred_rem=r))
+        b = O.chunk(data, O.Params(pred_mask=(1 << k) - 1, pred_value=r))
+        assert a[0].tolist() == b[0].tolist() and a[1].tolist() == b[1].tolist()
+    p = O.Params(pred_kind=O.PRED_DIV, pred_div=4099, pred_rem=7)
+    st, ln, dg = O.chunk(data, p)
+    assert st.tolist() != O.chunk(data)[0].tolist()
+    ref = O.py_chunk(data[:60000], p)
+    st2, ln2, dg2 = O.chunk(data[:60000], p)
+    assert [(int(a), int(b), d.tobytes()) for a, b, d in zip(st2, ln2, dg2)] == ref
+    # Java long remainder of the (non-negative) window fp: the candidates are exactly the positions
+    # whose definitional GF(2) fingerprint leaves remainder R
+    fps = O.window_fps(data[:5000])
+    for k in range(0, 5000, 97):
+        fp = O.gf2_window_fp(data, k)
+        assert int(fps[k]) == fp and p.is_boundary(fp) == (fp % 4099 == 7)
