@@ -930,3 +930,26 @@ def test_piece_mode_sections_joined_and_stitched():
         c = int(ec[b])
         assert counts[b] == c and (st[b, :c] == es[b, :c]).all() and (ln[b, :c] == el[b, :c]).all(), b
         assert (dg[b, :c] == ed[b, :c]).all(), b
+
+
+def test_jar_fixtures_bit_exact():
+    """tests/golden/jar_cdc.json, when present, holds the rabinwindow jar's OWN chunk lists for the
+    inputs of cdc.json (tools/java/JarParity.java --emit on a host with a JDK and the jar; absent in
+    this image).  Every fixture whose knob setting reproduces the jar's list is then run on the GPU
+    with that setting and must equal the jar — boundary parity pinned to the reference itself."""
+    import os
+
+    path = os.path.join(G.GOLDEN, "jar_cdc.json")
+    if not os.path.exists(path):
+        pytest.skip("no jar_cdc.json: the rabinwindow jar has not been run (INTEGRATION.md §4)")
+    jar = {f["name"]: f for f in G.load("jar_cdc.json")["fixtures"]}
+    matched = 0
+    for fx in G.fixtures():
+        j = jar.get(fx["name"])
+        if j is None or (j["starts"], j["lens"], j["digests"]) != (fx["starts"], fx["lens"], fx["digests"]):
+            continue
+        matched += 1
+        data = G.fixture_input(fx)
+        got = engine_for(fx["params"]).chunk_arrays(data)
+        assert_same(got, (j["starts"], j["lens"], [bytes.fromhex(h) for h in j["digests"]]), fx["name"])
+    assert matched > 0, "no knob setting of cdc.json reproduces the jar: add its detector to make_golden.py"

@@ -171,3 +171,18 @@ def test_divisor_detector_power_of_two_is_the_mask_and_others_differ():
     for k in range(0, 5000, 97):
         fp = O.gf2_window_fp(data, k)
         assert int(fps[k]) == fp and p.is_boundary(fp) == (fp % 4099 == 7)
+
+
+def test_java_parity_harness_generates_the_fixture_inputs():
+    """tools/java/JarParity.java (run where a JDK and the jar exist) must rebuild cdc.json's inputs
+    with the same generator: its SplitMix64 constants, stream key and default seed are the oracle's,
+    and it knows every input kind make_golden.py uses."""
+    import os
+    src = open(os.path.join(os.path.dirname(G.GOLDEN), "..", "tools", "java", "JarParity.java")).read()
+    for const in ("0x9E3779B97F4A7C15L", "0xBF58476D1CE4E5B9L", "0x94D049BB133111EBL", "0xD1B54A32D192ED03L",
+                  "0x5DF50001L", ">>> 30", ">>> 27", ">>> 31"):
+        assert const in src, const
+    kinds = {fx["input"]["kind"] for fx in G.fixtures()}
+    for k in kinds:
+        assert f'case "{k}"' in src, k
+    assert O.SYNTH_SEED == 0x5DF50001 and G.load("cdc.json")["seed"] == O.SYNTH_SEED
