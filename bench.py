@@ -36,20 +36,30 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz int32 ops/s
-# VALU instructions per input byte per lane (SQ_INSTS_VALU / (bytes / 64), rocprofv3 PMC of the
-# production kernels, profiles/r02/end/pmc_summary.json): scan 9.17 (10.8 before the bit-reversed
-# rolling state, the SGPR-mask candidate bits and the queue cut walk), SHA-256 22.3 (~1 420 per
-# 64-byte block incl. one padding block per chunk)
-OPS_PER_BYTE = {"cdc_scan": 9.17, "chunk_hash": 22.3}
-# SIMD issue cycles per wave-byte: the ISA mix of each kernel's loop weighted by the measured issue
-# cost of each instruction (scripts/isa_microbench.hip, profiles/r01/isa_microbench.txt: 2.0 for
-# xor/and/shift, 2.2 bitop3, 2.4 add/addc, 3.6 alignbit/perm/add3); the clock the microbenchmark
-# calibrates to under full VALU load is 2.07 GHz.  valu_busy = issue cycles / (SIMDs x clock x time).
-# scan: 21.5 in the 256-byte block body + ~1.5 for the walk and block overhead
-VALU_CYCLES_PER_BYTE = {"cdc_scan": 23.0, "chunk_hash": 4180.0 / 64 * 1.008}
-SIMDS, VALU_CLOCK_HZ = 256 * 4, 2.07e9
+# The fingerprint kernel is bound by VALU issue, not by HBM: its SHA-256 compression runs at the
+# issue rate of its own instruction mix (scripts/valu_issue_mb.hip, profiles/r05/valu_issue/: real
+# cycles per wave64 instruction per SIMD, 2.4 for xor/add/shift, ~2.5 bitop3, ~4.2 alignbit/add3/perm,
+# 3.9 for the compression's mix at 4 waves per SIMD; no order, register assignment or ILP form of the
+# round beats it).  The ceiling is measured live (sha_ceiling below) and the roofline reports the
+# kernel's compressed bytes per second against it next to the HBM fraction.
+PROBE_LIB = os.path.join(ROOT, "tools", "libsdfs_probe.so")
 METRIC = "device-resident GiB/s CDC+fingerprint, 4 KiB-mean chunks, 1/2/4/8 MI355X"
+
+
+def sha_ceiling(local: int, waves_per_simd: int = 4) -> float:
+    """GB/s of 64-byte blocks the production sha256_compress reaches register-only on every CU of
+    this GPU, now, at chunk_hash's occupancy (4 waves per SIMD: 120 VGPRs): the VALU issue ceiling
+    of the fingerprint (tools/probe_kernels.hip, a measurement library beside the product)."""
+    import ctypes
+
+    lib = ctypes.CDLL(PROBE_LIB)
+    f = lib.sdfs_probe_sha256_ceiling
+    f.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_double)] * 2
+    g, ms = ctypes.c_double(), ctypes.c_double()
+    rc = f(local, waves_per_simd, 200, 5, ctypes.byref(g), ctypes.byref(ms))
+    if rc:
+        raise RuntimeError(f"sdfs_probe_sha256_ceiling failed: {rc}")
+    return g.value
 
 
 def log(*a):
@@ -312,7 +322,7 @@ def main_device_set(args):
             "parallelism": f"device set of {n} GPUs in one process (streams sharded per GPU)",
         },
         "kernels_ms": {"chunk_hash_per_gpu": [round(x, 4) for x in hash_ms]},
-        "roofline": {"bound": "hbm", "kernel": "chunk_hash", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+        "roofline": {"bound": "valu", "kernel": "chunk_hash", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src},
         "cpu_baseline": None,
@@ -462,8 +472,10 @@ def main():
     torch.cuda.synchronize()
     kt = eng.kernel_times()
     eng.set_timing(0)
-    kt_one = dict(kt)
     counts, _, _, _, total = batch.host_results()
+    # what chunk_hash compresses per launch: every chunk's 64-byte blocks incl. its padding block(s)
+    valid = torch.arange(batch.cap, device=batch.lens.device)[None, :] < batch.counts[:, None]
+    sha_blocks = int((((batch.lens.view(nbuf, batch.cap).to(torch.int64) + 8) // 64 + 1) * valid).sum().item())
 
     # The roofline's launch duration: chunk_hash timed with HIP events over a one-stream timed
     # region (every step stream-ordered, so no other kernel shares the GPU with chunk_hash and its
@@ -497,6 +509,7 @@ def main():
                      "ms_per_step": round(el / args.steps * 1e3, 4)}
     if world > 1:
         other = None
+    ceiling = sha_ceiling(local)  # right after the one-stream region: the same clock regime
 
     # the other chunk mix beside the headline: the reference default (minLen 4095, 12-bit) when
     # the headline is the metric's 4 KiB-mean mix (minLen 2047, 11-bit), and vice versa
@@ -584,10 +597,6 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     # the roofline's kernel time cannot exceed the step it is part of
     assert 0 < hash_ms_one <= ms_step, f"chunk_hash {hash_ms_one:.3f} ms per launch > {ms_step:.3f} ms per step"
-    valu = {k: round(nbytes * OPS_PER_BYTE[k] / (kt_one[k] / 1e3) / VALU_PEAK_OPS, 3) for k in OPS_PER_BYTE
-            if kt_one.get(k)}
-    valu_busy = {k: round(nbytes / 64 * VALU_CYCLES_PER_BYTE[k] / (SIMDS * VALU_CLOCK_HZ * kt_one[k] / 1e3), 3)
-                 for k in VALU_CYCLES_PER_BYTE if kt_one.get(k)}
     params = (f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
               f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen {args.hash_type}")
     traffic, traffic_src = load_traffic("chunk_hash", params)
@@ -634,7 +643,7 @@ def main():
         "kernels_ms": {k: round(v, 4) for k, v in kt.items()},
         "kernels_note": "every stage: HIP events around each kernel in a separate untimed one-stream pass",
         "roofline": {
-            "bound": "hbm",
+            "bound": "valu",
             "kernel": "chunk_hash",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
@@ -649,8 +658,17 @@ def main():
             "two_stream_launch_ms": round(hash_ms_live, 4) if nsf >= 2 else None,
             "achieved_per_step": round(nbytes / (ms_step / 1e3) / 1e9, 1),
             "frac_per_step": round(nbytes / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-            "valu_frac": valu,
-            "valu_busy": valu_busy,
+            "valu": {
+                "ceiling_gbps": round(ceiling, 1),
+                "achieved_gbps": round(sha_blocks * 64 / t_dom / 1e9, 1),
+                "frac": round(sha_blocks * 64 / t_dom / 1e9 / ceiling, 4),
+                "unit": "GB/s of 64-byte SHA-256 blocks (chunk bytes + padding blocks)",
+                "sha_blocks_per_launch": sha_blocks,
+                "ceiling_source": ("production sha256_compress, register-resident data, every CU at 4 waves/SIMD, "
+                                   "timed in this process (tools/probe_kernels.hip)"),
+                "note": ("the kernel is bound by VALU issue of its SHA-256 instruction mix, not by HBM: frac above "
+                         "is of the 8 TB/s HBM peak, this one of the measured issue ceiling"),
+            },
         },
         "cpu_baseline": cpu,
         ("one_stream" if nsf >= 2 else "two_streams"): other,
