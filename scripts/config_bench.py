@@ -7,9 +7,10 @@ CONFIG=dedup  (configs[2]): 8 GiB = 32768 write buffers of 256 KiB, 50 % of them
               (CDC + SHA-256), the dedup-hit index (fresh per step), and the SparseDataChunk
               map images; LZ4 of the new chunks is timed beside it (on for compressed volumes).
 CONFIG=backup (configs[4], one GPU's slice): BACKUP_VOLUME=true: 102 write buffers of 40 MiB
-              (3.98 GiB), maxLen 128 KiB, tar-like stream (512-byte headers, file bodies of
-              log-uniform length, 20 % of bodies repeating an earlier one); one step = getChunks
-              + the index + LZ4 of the new chunks (backup volumes compress).
+              (3.98 GiB), maxLen 128 KiB, tar-like stream (sdfs_amd.device.tar_layout: 512-byte
+              headers, file bodies of log-uniform length zero-padded to 512, 20 % of bodies
+              repeating an earlier one); one step = getChunks + the index + LZ4 of the new chunks
+              (backup volumes compress).
 Stage times are HIP events on the launch stream, averaged over STEPS steps.  One JSON line."""
 import json
 import os
@@ -49,26 +50,12 @@ def fill_dedup(batch, nbuf, L, rng):
 
 
 def fill_backup(batch, total, rng):
-    """512-byte headers + bodies of log-uniform length 1 KiB..64 MiB; 20 % repeat an earlier body."""
-    data = batch.data
-    st = torch.cuda.current_stream().cuda_stream
-    p, k, bodies = 0, 0, []
-    while p < total:
-        h = min(512, total - p)  # header: 512 synthetic bytes
-        batch.engine.synth_device(data.data_ptr() + p, h, 0x7A5, 10**6 + k, 0, stream=st)
-        p += h
-        n = int(min(2 ** rng.uniform(10, 26), total - p))
-        if n <= 0:
-            break
-        if bodies and rng.random() < 0.2:
-            s0, sn = bodies[int(rng.integers(0, len(bodies)))]
-            n = min(n, sn, total - p)
-            data[p:p + n].copy_(data[s0:s0 + n].clone())
-        else:
-            batch.engine.synth_device(data.data_ptr() + p, n, 0x7A5, k, 0, stream=st)
-            bodies.append((p, n))
-        p += n
-        k += 1
+    """The tar-like stream of configs[4] (sdfs_amd.device.tar_layout: 512-byte headers, log-uniform
+    1 KiB-64 MiB bodies zero-padded to 512, 20 % of bodies repeating an earlier one), the same
+    generator tests/test_gpu_parity.py::test_config4_tar_stream_per_gpu_share_16gib checks."""
+    from sdfs_amd.device import tar_layout
+
+    batch.fill_tar(tar_layout(total))
     torch.cuda.synchronize()
 
 

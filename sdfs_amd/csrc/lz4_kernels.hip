@@ -403,6 +403,126 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(Lz4Args a) {
     }
 }
 
+// ---- literal screen (round 5).  Most chunks of a backup stream's file bodies are incompressible,
+// and for them LZ4's parse finds no match: every probe of the search (positions 1 + probe_off(i),
+// the step growing every 64 misses) compares its 4 bytes with the table's candidate, which is
+// either position 0 (the table starts zeroed, and position 0 is put first) or an EARLIER probe
+// position.  So when the 4-byte words at position 0 and at every probe position the parse makes
+// are pairwise distinct, no compare can succeed, the parse runs to its end, and the block is the
+// chunk as one literal run (last_literals with anchor 0) — whatever the mode (R123 / V19 differ in
+// the search end, which sets the probe count, and in hashing, which does not matter here).  The
+// screen checks exactly that, one wave per chunk: the words go into an LDS hash set (linear
+// probing, compare-and-swap); a chunk with all words distinct is written as its literal block, any
+// other chunk (a repeated word: compressible, or an accidental repeat) joins the `rest` list that
+// the exact kernels then run on.  Output is the same bytes either way (tests/test_lz4.py).
+constexpr uint32_t kScreenSlots = 4096;  // LDS set of one one-wave workgroup (16 KiB)
+constexpr uint32_t kScreenMaxWords = kScreenSlots / 2;  // load factor <= 1/2 (~32 KiB chunks)
+constexpr int kScreenWgPerCu = 9;
+
+// Probes the search makes in a chunk without a match: probe i is made iff the next position,
+// 1 + probe_off(i + 1), is <= search_end; returns their count P (probes 0 .. P-1).
+__device__ __forceinline__ uint32_t screen_probes(uint32_t search_end) {
+    if (search_end < 2) return 0;  // 1 + probe_off(1) = 2
+    uint32_t lo = 1, hi = 1u << 16;  // 1 + probe_off(2^16) > 2^27 > any screened chunk
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (1 + probe_off(mid) <= search_end) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void lz4_literal_screen_kernel(Lz4Args a, uint32_t* rest) {
+    __shared__ __attribute__((aligned(16))) uint32_t set[kScreenSlots];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t n_items = a.d_count ? min<uint64_t>(*a.d_count, a.n_max) : a.n_max;
+    for (uint64_t i = blockIdx.x; i < n_items; i += gridDim.x) {
+        const uint64_t c = a.idx ? a.idx[i] : i;
+        const uint32_t n = a.src_len[c];
+        const uint8_t* src = a.data + a.src_off[c];
+        bool literal = n < kMfLimit + 1;  // too short to search: literals only
+        if (!literal && n < (1u << 27)) {
+            const uint32_t mflimit = n - kMfLimit;
+            const uint32_t search_end = MODE == SDFS_CDC_LZ4_V19 ? mflimit + 1 : mflimit;
+            const uint32_t P = screen_probes(search_end);
+            // words: position 0, the P probe positions, and (harmless: at worst a false repeat)
+            // the first position past the search while it is inside the chunk
+            const uint32_t nw = 1 + P + (1 + probe_off(P) + 4 <= n ? 1u : 0u);
+            if (nw <= kScreenMaxWords) {
+                uint32_t lg = 6;
+                while ((1u << lg) < 2 * nw) lg++;
+                const uint32_t mask = (1u << lg) - 1;
+                for (uint32_t s = lane; 4 * s <= mask; s += 64) reinterpret_cast<uint4*>(set)[s] = make_uint4(0, 0, 0, 0);
+                __syncthreads();
+                bool dup = false;
+                uint32_t zeros = 0;  // the word 0 is the set's empty mark: counted instead
+                // a first round of one word per lane (compressible chunks show a repeat there and
+                // leave early), then eight per lane
+                for (uint32_t k0 = 0, per = 1; k0 < nw && !dup; k0 += 64 * per, per = 8) {
+                    uint32_t v[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const uint32_t k = k0 + 64 * j + lane;
+                        v[j] = 0xFFFFFFFFu;
+                        if ((uint32_t)j < per && k < nw) v[j] = g32(src + (k == 0 ? 0u : 1 + probe_off(k - 1)));
+                    }
+                    // first probe of every word in straight-line code (eight compare-and-swaps in
+                    // flight); only a word whose slot holds another word walks on (rare at load <= 1/2)
+                    uint32_t sl[8], old[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const uint32_t k = k0 + 64 * j + lane;
+                        const bool ok = (uint32_t)j < per && k < nw && v[j] != 0;
+                        zeros += (uint32_t)j < per && k < nw && v[j] == 0;
+                        sl[j] = (v[j] * 2654435761u) >> (32 - lg);
+                        old[j] = ok ? atomicCAS(&set[sl[j]], 0u, v[j]) : 0u;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        dup = dup || (old[j] != 0 && old[j] == v[j]);
+                        if (old[j] != 0 && old[j] != v[j]) {
+                            uint32_t t = sl[j];
+                            for (;;) {
+                                t = (t + 1) & mask;
+                                const uint32_t o2 = atomicCAS(&set[t], 0u, v[j]);
+                                if (o2 == 0) break;
+                                if (o2 == v[j]) {
+                                    dup = true;
+                                    break;
+                                }
+                            }
+                        }
+                    }
+                    dup = __any(dup) || __any(zeros > 1) || __popcll(__ballot(zeros > 0)) > 1;
+                }
+                literal = !dup;
+                __syncthreads();  // the set is cleared again only after every lane is done with it
+            }
+        }
+        if (!literal) {
+            if (lane == 0) rest[1 + atomicAdd(rest, 1u)] = (uint32_t)c;
+            continue;
+        }
+        uint8_t* o = a.out + a.dst_off[c];
+        const uint32_t hdr = a.framed ? 4u : 0u;
+        uint32_t op = hdr;
+        if (lane == 0) {
+            if (hdr) {
+                o[0] = (uint8_t)(n >> 24);
+                o[1] = (uint8_t)(n >> 16);
+                o[2] = (uint8_t)(n >> 8);
+                o[3] = (uint8_t)n;
+            }
+            o[hdr] = (uint8_t)((n >= kRunMask ? kRunMask : n) << 4);
+        }
+        op++;
+        if (n >= kRunMask) op = put_run(o, op, n - kRunMask, lane);
+        copy_bytes(o + op, src, n, lane);
+        if (lane == 0) a.dst_len[c] = op + n;
+    }
+}
+
 // ---- decompression (the read side: HashBlobArchive.getChunk -> CompressionUtils.decompressLz4,
 // HashBlobArchive.java:1927-1933, CompressionUtils.java:122-125; LZ4 block format).  One wave per
 // block: the token stream is parsed as wave-uniform scalar work, literal runs are copied 16 bytes
@@ -1070,6 +1190,8 @@ struct sdfs_cdc_lz4 {
     int lane_wg_per_cu = 4;       // SDFS_LZ4_LANE_WG_PER_CU: 256-thread workgroups per CU (lane mode)
     ZBuf<uint32_t> ltag;
     ZBuf<uint32_t> bail;          // hybrid (lane_mode 2): count + bailed chunk indices
+    int screen = 1;               // literal screen before the exact kernels (SDFS_LZ4_SCREEN=0: off, tuning build)
+    ZBuf<uint32_t> rest;          // screen: count + the chunks the exact kernels compress
     uint32_t bail_misses = 128;   // SDFS_LZ4_BAIL
     int lane_sort = 0;            // SDFS_LZ4_LANE_SORT=1: lanes take chunks longest first (measured slower)
     int lane_depth = kLaneDepth;  // SDFS_LZ4_LANE_DEPTH
@@ -1162,7 +1284,22 @@ int launch_compress(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
     return rc ? rc : rr;
 }
 
-int launch_compress_impl(sdfs_cdc_lz4* z, const Lz4Args& a, hipStream_t s) {
+int launch_compress_impl(sdfs_cdc_lz4* z, const Lz4Args& a0, hipStream_t s) {
+    // The literal screen first (every batch): chunks whose parse can find no match are written as
+    // one literal run here; the exact kernels below run on the `rest` list only.
+    Lz4Args a = a0;
+    if (z->screen && !a0.idx) {
+        LZ_TRY(z->rest.ensure(a0.n_max + 1));
+        LZ_TRY(hipMemsetAsync(z->rest.p, 0, 4, s));
+        const uint32_t sgrid = (uint32_t)std::min<uint64_t>(a0.n_max, (uint64_t)z->num_cus * kScreenWgPerCu);
+        if (z->mode == SDFS_CDC_LZ4_V19)
+            hipLaunchKernelGGL(lz4_literal_screen_kernel<SDFS_CDC_LZ4_V19>, dim3(sgrid), dim3(64), 0, s, a0, z->rest.p);
+        else
+            hipLaunchKernelGGL(lz4_literal_screen_kernel<SDFS_CDC_LZ4_R123>, dim3(sgrid), dim3(64), 0, s, a0, z->rest.p);
+        LZ_TRY(hipGetLastError());
+        a.d_count = z->rest.p;
+        a.idx = z->rest.p + 1;
+    }
     // Auto: a batch with enough chunks to fill the chip one lane per chunk runs the hybrid (lanes
     // for compressible chunks, the wave kernel for the ones a lane bails on); smaller batches the
     // wave kernel (scripts/probes/lz4_batch_sweep.sh: the hybrid pays from ~50 000 chunks per 256 CUs).
@@ -1273,6 +1410,7 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     if (const char* v = getenv("SDFS_LZ4_LANE_SORT")) z->lane_sort = atoi(v);
     if (const char* v = getenv("SDFS_LZ4_LANE_DEPTH")) z->lane_depth = atoi(v);
     if (const char* v = getenv("SDFS_LZ4_PRETEST")) z->pretest = atoi(v);
+    if (const char* v = getenv("SDFS_LZ4_SCREEN")) z->screen = atoi(v);
 #endif
     if (hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess) {
         delete z;
@@ -1297,6 +1435,7 @@ int sdfs_cdc_lz4_destroy(sdfs_cdc_lz4* z) {
         z->gtab.release();
         z->ltag.release();
         z->bail.release();
+        z->rest.release();
         z->ord.release();
         z->h_in.release();
         z->h_out.release();

@@ -371,3 +371,40 @@ def test_gpu_large_batch_hybrid_vs_oracle():
         torch.cuda.synchronize()
         assert torch.equal(blen, src_len) and torch.equal(back, batch.data)
     e.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [Z.R123, Z.V19], ids=["r123", "v19"])
+def test_gpu_literal_screen_edges_vs_oracle(mode):
+    """The literal screen (lz4_kernels.hip: a chunk whose words at position 0 and at every search
+    probe are pairwise distinct is one literal run) against the oracle's parse on its edges: random
+    chunks (screened), random chunks with one 4-byte word planted again at a probe position or at a
+    position the search skips (a repeat the screen must send to the exact kernels, or need not),
+    a repeat of position 0's word, zero words (the set's empty mark), chunks right at the search's
+    end (13 .. 16 bytes) and long ones (u32 tables, more probes than the LDS set holds)."""
+    rng = np.random.default_rng(55 + mode)
+    parts = []
+    for i in range(400):
+        n = int(rng.choice([13, 14, 15, 16, 17, 64, 100, 4096, 8192, 20000, 32768, 65547, 131072]))
+        d = bytearray(C.synth(9, 2000 + i, 0, n).tobytes())
+        kind = i % 5
+        if kind == 1 and n > 40:  # a word planted again further on (at a probe or a skipped position)
+            a = int(rng.integers(0, n // 2))
+            b = int(rng.integers(a + 4, n - 4))
+            d[b:b + 4] = d[a:a + 4]
+        elif kind == 2 and n > 40:  # position 0's word again
+            b = int(rng.integers(1, n - 4))
+            d[b:b + 4] = d[0:4]
+        elif kind == 3 and n > 40:  # a zero word, or two
+            for _ in range(int(rng.integers(1, 3))):
+                b = int(rng.integers(0, n - 4))
+                d[b:b + 4] = b"\0\0\0\0"
+        parts.append(bytes(d))
+    lens = np.array([len(p) for p in parts], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 1)]).astype(np.uint64)
+    base = np.zeros(int(offs[-1]) + int(lens[-1]) + 8, np.uint8)
+    for o, p in zip(offs, parts):
+        base[int(o): int(o) + len(p)] = np.frombuffer(p, np.uint8)
+    got = comp(mode).compress_chunks(base, offs, lens, framed=True)
+    for i, p in enumerate(parts):
+        assert got[i] == Z.compress_framed(p, mode), (i, len(p), i % 5)
