@@ -223,11 +223,13 @@ __global__ __launch_bounds__(256) void cdc_resolve_lds_kernel(ResolveArgs a) {
         const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
         const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
         const uint32_t r0 = SPEC ? (item - b * a.nsec) * a.sec_len : 0;
-        if (r0 >= len) {  // workgroup-uniform: section past this buffer's end
-            if constexpr (SPEC) {
-                if (threadIdx.x == 0) {
+        if (r0 >= len) {  // workgroup-uniform: section past this buffer's end (or an empty buffer)
+            if (threadIdx.x == 0) {
+                if constexpr (SPEC) {
                     a.spec_cnt[item] = 0;
                     a.spec_next[item] = len;
+                } else {
+                    a.counts[b] = 0;
                 }
             }
             continue;
