@@ -196,3 +196,84 @@ def test_shard_of_matches_rocksdb_rule():
         if l < 0:
             l = (l * -1) + 127
         assert got[b] == l // 32, b
+
+
+# ---- configs[3] shape with CHUNKED records: every rank chunks its shard of the write streams
+# (the oracle standing in for the engine on the CPU), builds the engine's 48-byte records
+# {digest[32], u64 buffer_id, u32 start, u32 len} with bench.py's buffer ids (rank * nbuf + local),
+# and exchanges them through RecordExchange (direct slots, 3 steps, as bench.py at N > 1).  Every
+# rank must end with the global table in (rank, buffer, chunk) order, each step.
+_S, _BPS, _BL = 2, 2, 65536  # streams per rank, buffers per stream and step, buffer length
+
+
+def _rank_records(rank, world, step):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    from oracle import cdc_oracle as O
+    streams = shard_streams(_S * world, world, rank)
+    nbuf = len(streams) * _BPS
+    out = bytearray()
+    for k, s in enumerate(streams):
+        for j in range(_BPS):
+            data = O.synth_c(O.SYNTH_SEED, s, (step * _BPS + j) * _BL, _BL)
+            st, ln, dg = O.chunk(data, O.Params())
+            bid = rank * nbuf + k * _BPS + j
+            for i in range(len(st)):
+                out += dg[i].tobytes() + bid.to_bytes(8, "little") + int(st[i]).to_bytes(4, "little") + \
+                    int(ln[i]).to_bytes(4, "little")
+    return bytes(out)
+
+
+def _chunked_exchange_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cap = _S * _BPS * (_BL // 4096 + 2)  # the engine's slot capacity bound per buffer, summed
+        ex = RecordExchange(cap, "cpu", depth=2, slots=3)
+        for step in range(3):
+            recs = _rank_records(rank, world, step)
+            n = len(recs) // RECORD_BYTES
+            table = ex.acquire()
+            table[:] = 255  # garbage beyond the count must not travel
+            table[:n] = torch.frombuffer(bytearray(recs), dtype=torch.uint8).view(n, RECORD_BYTES)
+            ex.submit(table, torch.tensor([n]))
+        got = ex.flush()
+        q.put((rank, [(RecordExchange.compact(g, cl).numpy().tobytes(), cl) for g, cl in got]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_configs3_chunked_records_exchange_gloo(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_chunked_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    nbuf = _S * _BPS
+    for step in range(3):
+        per_rank = [_rank_records(r, world, step) for r in range(world)]
+        expect = b"".join(per_rank)
+        for r in range(world):
+            rows, counts = res[r][step]
+            assert counts == [len(x) // RECORD_BYTES for x in per_rank]
+            assert rows == expect, (r, step)
+        # the gathered table covers every buffer of every rank exactly, in order
+        recs = memoryview(expect)
+        cover = {}
+        for i in range(len(expect) // RECORD_BYTES):
+            rec = recs[i * RECORD_BYTES:(i + 1) * RECORD_BYTES]
+            bid = int.from_bytes(rec[32:40], "little")
+            st = int.from_bytes(rec[40:44], "little")
+            ln = int.from_bytes(rec[44:48], "little")
+            assert st == cover.get(bid, 0)
+            cover[bid] = st + ln
+        assert cover == {b: _BL for b in range(world * nbuf)}
