@@ -37,10 +37,15 @@ $(TUNING_LIB): $(TUNING_OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,-z,defs -o $@ $(TUNING_OBJS) -ldl
 
 # host-side harnesses: the multi-threaded getChunks driver (bench.py, GPU tests) and the JNI glue
-tools: tools/libsdfs_threads.so tools/libsdfs_probe.so jni/libsdfs_cdc_jni.so tests/jni/libjni_stub.so
+tools: tools/libsdfs_threads.so tools/libsdfs_threads_tuning.so tools/libsdfs_probe.so jni/libsdfs_cdc_jni.so tests/jni/libjni_stub.so
 
 tools/libsdfs_threads.so: tools/threads_bench.c include/sdfs_cdc.h $(LIB)
 	gcc -O2 -std=c11 -fPIC -shared -Wl,-z,defs -Wall -Wextra -D_GNU_SOURCE -o $@ $< -Lsdfs_amd -lsdfs_cdc -Wl,-rpath,'$$ORIGIN/../sdfs_amd' -lpthread
+
+# the same harness against the tuning library (scripts/ with SDFS_CDC_LIB=...tuning.so: an engine
+# handle is only valid in the library that made it)
+tools/libsdfs_threads_tuning.so: tools/threads_bench.c include/sdfs_cdc.h $(TUNING_LIB)
+	gcc -O2 -std=c11 -fPIC -shared -Wl,-z,defs -Wall -Wextra -D_GNU_SOURCE -o $@ $< -Lsdfs_amd -lsdfs_cdc_tuning -Wl,-rpath,'$$ORIGIN/../sdfs_amd' -lpthread
 
 # measurement-only kernels bench.py runs beside the product library (the fingerprint's VALU ceiling)
 tools/libsdfs_probe.so: tools/probe_kernels.hip $(HDRS)

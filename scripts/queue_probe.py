@@ -11,13 +11,19 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from sdfs_amd import HipVariableSha256HashEngine  # noqa: E402
+from sdfs_amd import HipVariableSha256HashEngine, SdfsConfig  # noqa: E402
 from sdfs_amd.device import DeviceBatch  # noqa: E402
 from tools import threads as T  # noqa: E402
 
 L = 262144
 nb = 1024
-e0 = HipVariableSha256HashEngine()
+# MASK_BITS=11 MIN_SEG_KIB=2: the bench's 4 KiB-mean mix (default: the reference defaults)
+MODE = os.environ.get("MODE", "copy")  # "fill": the JNI glue's entry (sdfs_cdc_get_chunks_fill)
+cfg = SdfsConfig()
+if os.environ.get("MASK_BITS"):
+    cfg = SdfsConfig(min_len=int(os.environ.get("MIN_SEG_KIB", "4")) * 1024 - 1,
+                     pred_mask=(1 << int(os.environ["MASK_BITS"])) - 1)
+e0 = HipVariableSha256HashEngine(config=cfg)
 b = DeviceBatch(e0, nbuf=nb, buf_len=L)
 b.fill_streams(0, 64)
 torch.cuda.synchronize()
@@ -34,12 +40,14 @@ def cpu_stat():
 
 
 for th in [int(x) for x in os.environ.get("THREADS", "1,32,128,384").split(",")]:
-    e = HipVariableSha256HashEngine()
-    T.getchunks(e, th, host, L, max(256, 4 * th))  # warm: every slot and lane carries a pass
+    e = HipVariableSha256HashEngine(config=cfg)
+    T.getchunks(e, th, host, L, max(256, 4 * th), mode=MODE)  # warm: every slot and lane carries a pass
     b0 = e.queue_stats()
     c0 = cpu_stat()
     calls = max(256, th * 8)
-    r, _ = T.getchunks(e, th, host, L, calls)
+    r, _ = T.getchunks(e, th, host, L, calls, mode=MODE)
+    if r.first_error:
+        raise SystemExit(f"getChunks failed at {th} threads: status {r.first_error}")
     c1 = cpu_stat()
     b1 = e.queue_stats()
     thr = {k: c1[k] - c0.get(k, 0) for k in ("nr_throttled", "throttled_usec", "usage_usec") if k in c1}

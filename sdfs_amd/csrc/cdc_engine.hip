@@ -161,9 +161,10 @@ constexpr int kEvPerRun = 2 * 8;
 // recorded after its previous run (cross-stream wait, no host sync).
 constexpr uint32_t kSmall = 2 * kMaxBins + 8;  // hist | cursor | overflow, total, wave_ctr ..
 constexpr int kRing = 3;
-constexpr int kQueueInflight = 4;  // coalescing-queue lanes: batches on the device at once, one stream each
-                                   // (GPU_MAX_HW_QUEUES is 4: more streams would share hardware queues)
-constexpr int kQueueSlots = 8;
+constexpr int kQueueInflight = 4;  // coalescing-queue lane streams (the most lanes a queue can run)
+constexpr int kQueueLanes = 4;     // lanes: batches on the device at once, one stream each (8 lanes
+                                   // measured slower: smaller passes, profiles/r05/queue/lanes_4_vs_8)
+constexpr int kQueueSpareSlots = 4;  // slots beyond one per lane: the open one and the ones being read
 struct Workspace {
     DevBuf<uint32_t> bitmap;
     DevBuf<uint64_t> seg_prefix;
@@ -207,11 +208,13 @@ struct HostSlot {
 
 // Device state of one coalescing-queue slot (host_queue.h): the batch's device copy, and its
 // result image, written by the kernels in place on the device (dimg) and copied to pinned host
-// memory (pin_out) in ONE transfer once the kernels are done:
+// memory (pin_out) in ONE pass by the last kernel of the batch (copy_out_kernel):
 //   counts[n] | starts[n*dcap] | lens[n*dcap] | flags[16] | digests[n*dcap*32] | hash digests[nh*32]
-// The copy back is issued by the completer after the kernels finished, not queued behind them at
-// launch: copies of every stream go through the same DMA queue in order, so a device->host copy
-// waiting on one batch's kernels would hold up the next batch's host->device copy.
+// The GPU writes the pinned image itself, in stream order behind the fingerprint: no DMA-engine
+// copy (copies of every stream share the DMA queues in order, so a device->host copy waiting on
+// one batch's kernels would hold up the next batch's host->device copy) and no host round trip
+// between the kernels and the copy (the completer used to issue it after waking on the kernels:
+// 27 us at 8 caller threads, 350 us at 48, profiles/r05/queue/).
 struct QSlotDev {
     uint8_t* pin_meta = nullptr;  // chunk offs u64[max_reqs] | lens u32 | hash offs u64 | lens u32
     size_t pin_meta_n = 0;
@@ -223,7 +226,7 @@ struct QSlotDev {
     DevBuf<uint32_t> total;
     DevBuf<uint8_t> dimg;     // device result image (pin_out's layout)
     Workspace ws;  // the slot's own pipeline scratch (a slot is reused only after its batch completed)
-    hipEvent_t kdone = nullptr;  // kernels of the batch done
+    hipEvent_t kdone = nullptr;  // kernels of the batch done (result image in pin_out)
     hipStream_t st = nullptr;    // the lane stream it runs on
     // layout of the batch in flight (read by the callers)
     uint32_t n = 0, nh = 0, dcap = 0;
@@ -1115,6 +1118,7 @@ struct QueueBackend {
                               d->dimg.p + d->hdig_at, st, &d->ws);
             if (rc) return rc;
         }
+        HIP_TRY(launch_copy_out(d->dimg.p, d->pin_out, d->img_bytes, st));
         HIP_TRY(hipEventRecord(d->kdone, st));
         return SDFS_CDC_OK;
     }
@@ -1127,13 +1131,10 @@ struct QueueBackend {
         return rc;
     }
 
-    // Kernels done -> one copy of the result image -> done.  The lane's stream carries no other
-    // batch meanwhile (one batch per lane in flight).
+    // Kernels (the last one wrote the pinned result image) done -> done.
     int wait_impl(QSlotDev* d) {
         HIP_TRY(hipSetDevice(e->prm.device));
         HIP_TRY(hipEventSynchronize(d->kdone));
-        HIP_TRY(hipMemcpyAsync(d->pin_out, d->dimg.p, d->img_bytes, hipMemcpyDeviceToHost, d->st));
-        HIP_TRY(hipStreamSynchronize(d->st));
         if (d->n) {
             const uint32_t* pflag = reinterpret_cast<const uint32_t*>(d->pin_out) + d->n + 2ull * d->n * d->dcap;
             if (*pflag) return fail(SDFS_CDC_EHIP, "internal: chunk slot overflow");
@@ -1153,14 +1154,31 @@ bool queue_ready(DevEngine* e) {
     // result image: room for every 64-byte-aligned request's worst-case chunk list at the
     // shortest chunk length, plus two slots of tail per request
     const uint64_t shortest = std::max<uint64_t>(1, std::min<uint64_t>(e->first_off + 1, e->prm.max_len));
+    {
+        // Queue lanes, created with the queue (an engine that never sees a single-buffer call holds
+        // no lane streams): each lane's passes are a long serial SHA-256 chain on a few CUs, so
+        // lanes must run side by side.  Streams beyond GPU_MAX_HW_QUEUES share hardware queues, and
+        // two lanes on one queue run their passes one after the other (the bench's process, where
+        // torch's streams came first: lanes on queues 3,4,4,3, 1.6 instead of 2.9 GiB/s at 8
+        // callers, profiles/r05/queue/).  A stream with a CU mask gets a hardware queue of its own;
+        // the mask is every CU.
+        if (hipSetDevice(e->prm.device) != hipSuccess) return false;
+        std::vector<uint32_t> mask((e->num_cus + 31) / 32, 0xFFFFFFFFu);
+        for (auto& q : e->qs)
+            if (!q && hipExtStreamCreateWithCUMask(&q, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+                q = nullptr;
+                e->q_state = -1;  // the direct path serves every call
+                return false;
+            }
+    }
     e->qb.reset(new QueueBackend{e, slot, 1024, slot / 2, slot / shortest + 2ull * 1024});
     CoalescingQueue<QueueBackend>::Config c;
-    c.nslots = kQueueSlots;
-    c.lanes = kQueueInflight;
+    c.lanes = kQueueLanes;
 #ifdef SDFS_TUNING
     if (const char* v = getenv("SDFS_Q_INFLIGHT")) c.lanes = std::max(1, std::min(atoi(v), kQueueInflight));
     if (const char* v = getenv("SDFS_Q_LINGER_US")) c.linger_us = (uint32_t)atoi(v);
 #endif
+    c.nslots = c.lanes + kQueueSpareSlots;
     c.max_reqs = 1024;
     c.max_req_bytes = slot / 2;
     e->q.reset(new CoalescingQueue<QueueBackend>(*e->qb, c));
@@ -1229,7 +1247,6 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     e->nbins = (maxblocks >> e->bin_shift) + 1;
     bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) == hipSuccess;
-    for (auto& q : e->qs) ok = ok && hipStreamCreateWithFlags(&q, hipStreamNonBlocking) == hipSuccess;
     for (auto& sl : e->hs)
         ok = ok && hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;

@@ -206,6 +206,7 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
 // latency form for small batches (SHA-256 / SHA-256/160 only): two waves per 64 chunks
 hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t stream);
 hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t stream);
+hipError_t launch_copy_out(const void* src, void* dst, uint64_t bytes, hipStream_t stream);
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
                         hipStream_t stream);
 bool scan_window_supported(int window);

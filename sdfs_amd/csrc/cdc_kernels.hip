@@ -806,6 +806,25 @@ __global__ __launch_bounds__(256) void synth_kernel(uint8_t* out, uint64_t n, ui
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// result image -> pinned host memory, written by the GPU itself in stream order (the coalescing
+// queue's passes): no DMA-engine copy behind the kernels and no host round trip to issue one.
+// `dst` is device-accessible pinned host memory; n16 = bytes / 16.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void copy_out_kernel(const uint4* src, uint4* dst, uint64_t n16) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+hipError_t launch_copy_out(const void* src, void* dst, uint64_t bytes, hipStream_t s) {
+    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15))
+        return hipErrorInvalidValue;
+    const uint64_t n16 = bytes / 16;
+    if (n16 == 0) return hipSuccess;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n16 + 255) / 256, 1024);
+    hipLaunchKernelGGL(copy_out_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(src),
+                       reinterpret_cast<uint4*>(dst), n16);
+    return hipGetLastError();
+}
 
 // ------------------------------------------------------------------------------------------
 // 6. fingerprints of given extents (getHash in bulk): longest-first order of n chunk lengths

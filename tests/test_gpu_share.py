@@ -149,6 +149,7 @@ def test_device_set_all_gpus_batch_device_and_allgather():
             bt = DeviceBatch(e, nbuf=per, buf_len=L, device=f"cuda:{d}")
             bt.fill_streams(first_stream=9600 + 3 * d, bufs_per_stream=16)
             s = torch.cuda.Stream(device=d)
+            s.wait_stream(torch.cuda.current_stream(d))  # the fill ran on the current stream
             bt.run(buffer_id_base=d * per, stream=s.cuda_stream)
             batches.append(bt)
             streams.append(s)

@@ -10,6 +10,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libsdfs_threads.so")
+# linked against the library the engine handles come from (SDFS_CDC_LIB may select the tuning build)
+LIB_TUNING = os.path.join(HERE, "libsdfs_threads_tuning.so")
 
 
 class Result(ctypes.Structure):
@@ -30,7 +32,8 @@ def load():
     if _lib is None:
         from sdfs_amd import _lib as engine_lib
         engine_lib.load()  # the engine (and torch's HIP runtime) first
-        lib = ctypes.CDLL(LIB)
+        tuning = os.path.basename(engine_lib.LIB_PATH) == "libsdfs_cdc_tuning.so"
+        lib = ctypes.CDLL(LIB_TUNING if tuning else LIB)
         vp = ctypes.c_void_p
         lib.sdfs_threads_getchunks.argtypes = [vp, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                                ctypes.c_uint32, vp, vp, vp, vp, ctypes.POINTER(Result)]
