@@ -10,10 +10,10 @@
 //   free    the same instructions, but the push address is taken from a data dword: the LDS
 //           reads no longer sit on the loop-carried chain (only the VALU shift/xor chain does)
 //   valu    chain without the two LDS reads (register stand-ins, ABL 1|2: one extra shift each)
-//   lds     only the address SDWAs and the two reads per byte (+ one xor to keep them live)
 // Wall cycles per wave-byte per SIMD = kernel time x clock x 4 SIMDs x CUs / (waves x bytes).
 // If `free` runs near `chain`, the loop is bound by issue + LDS throughput (no ILP will help); if
-// it runs near max(valu, lds), the chain's latency is what costs.
+// it runs much faster, the chain's latency is what costs.  (An LDS-only form was dropped: hipcc
+// hoisted its reads into 128 VGPRs and the number measured that, not the LDS.)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/scan_mix_mb.hip -o scripts/bin/scan_mix_mb
 #include "../sdfs_amd/csrc/cdc_device.h"
 
@@ -42,19 +42,6 @@ __device__ __forceinline__ void roll_free(uint32_t& lo, uint32_t& hi, uint32_t d
     hi = xor3(nhi, pv.y, qv.x);
 }
 
-// FORM 3: the addresses and the reads only
-template <int Q>
-__device__ __forceinline__ void lds_only(uint32_t& acc, uint32_t odw, uint32_t ad, uint32_t& c8, uint32_t& push_base,
-                                         uint32_t jshift, const uint8_t* tab) {
-    asm("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-        : "+v"(push_base)
-        : "v"(ad), "s"(jshift));
-    sdwa_byte_to_b1<3 - Q>(c8, odw);
-    const uint2 pv = *reinterpret_cast<const uint2*>(tab + push_base);
-    const uint2 qv = *reinterpret_cast<const uint2*>(tab + c8);
-    acc = xor3(acc, pv.x ^ pv.y, qv.x ^ qv.y);
-}
-
 template <int O, int FORM>
 __device__ __forceinline__ void steps(uint32_t& lo, uint32_t& hi, uint32_t& bits, const uint32_t (&cur)[16],
                                       const uint32_t (&prev)[16], uint32_t& c8, uint32_t& pb, uint32_t jshift,
@@ -67,22 +54,18 @@ __device__ __forceinline__ void steps(uint32_t& lo, uint32_t& hi, uint32_t& bits
             roll_step<(O & 3), (OI & 3), kProdAbl>(lo, hi, cur[O >> 2], odw, c8, pb, jshift, tab);
         else if constexpr (FORM == 1)
             roll_free<(O & 3), (OI & 3)>(lo, hi, cur[O >> 2], odw, cur[(O * 5 + 3) & 15], c8, pb, jshift, tab);
-        else if constexpr (FORM == 2)
-            roll_step<(O & 3), (OI & 3), kProdAbl | 1 | 2>(lo, hi, cur[O >> 2], odw, c8, pb, jshift, tab);
         else
-            lds_only<(OI & 3)>(hi, odw, cur[(O * 5 + 3) & 15], c8, pb, jshift, tab);
-        if constexpr (FORM != 3) {
-            hv[O & 7] = hi;
-            if constexpr ((O & 7) == 7) {
-                uint32_t m = min(min(hv[0], hv[1]), hv[2]);
-                m = min(min(m, hv[3]), hv[4]);
-                m = min(min(m, hv[5]), hv[6]);
-                m = min(m, hv[7]);
-                if (__builtin_expect(__any(m < thr), 0))
-                    bits ^= m;
-                else
-                    bits <<= 8;
-            }
+            roll_step<(O & 3), (OI & 3), kProdAbl | 1 | 2>(lo, hi, cur[O >> 2], odw, c8, pb, jshift, tab);
+        hv[O & 7] = hi;
+        if constexpr ((O & 7) == 7) {
+            uint32_t m = min(min(hv[0], hv[1]), hv[2]);
+            m = min(min(m, hv[3]), hv[4]);
+            m = min(min(m, hv[5]), hv[6]);
+            m = min(m, hv[7]);
+            if (__builtin_expect(__any(m < thr), 0))
+                bits ^= m;
+            else
+                bits <<= 8;
         }
         if constexpr ((O & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         steps<O + 1, FORM>(lo, hi, bits, cur, prev, c8, pb, jshift, tab, hv, thr);
@@ -181,6 +164,5 @@ int main() {
     measure("chain (production)", k_scan<0>, it, cus, d_rec, sink);
     measure("free (push address from data)", k_scan<1>, it, cus, d_rec, sink);
     measure("valu (no LDS reads)", k_scan<2>, it, cus, d_rec, sink);
-    measure("lds (addresses + reads only)", k_scan<3>, it, cus, d_rec, sink);
     return 0;
 }
