@@ -161,9 +161,9 @@ constexpr int kEvPerRun = 2 * 8;
 // recorded after its previous run (cross-stream wait, no host sync).
 constexpr uint32_t kSmall = 2 * kMaxBins + 8;  // hist | cursor | overflow, total, wave_ctr ..
 constexpr int kRing = 3;
-constexpr int kQueueInflight = 4;  // coalescing-queue lane streams (the most lanes a queue can run)
-constexpr int kQueueLanes = 4;     // lanes: batches on the device at once, one stream each (8 lanes
-                                   // measured slower: smaller passes, profiles/r05/queue/lanes_4_vs_8)
+constexpr int kQueueInflight = 8;  // coalescing-queue lane streams (the most lanes a queue can run)
+constexpr int kQueueLanes = 4;     // lanes: batches on the device at once, one stream each (6 or 8
+                                   // measured no faster, profiles/r05/queue/lanes_cumask)
 constexpr int kQueueSpareSlots = 4;  // slots beyond one per lane: the open one and the ones being read
 struct Workspace {
     DevBuf<uint32_t> bitmap;
@@ -1055,7 +1055,7 @@ struct QueueBackend {
         std::lock_guard<std::mutex> lk(e->mu);
         auto* d = static_cast<QSlotDev*>(s.dev);
         d->err.clear();
-        hipStream_t st = e->qs[lane % kQueueInflight];
+        hipStream_t st = e->qs[lane];  // lane < Config::lanes: created by queue_ready
         d->st = st;
         const int rc = launch_impl(s, d, st);
         if (rc) {
@@ -1154,24 +1154,6 @@ bool queue_ready(DevEngine* e) {
     // result image: room for every 64-byte-aligned request's worst-case chunk list at the
     // shortest chunk length, plus two slots of tail per request
     const uint64_t shortest = std::max<uint64_t>(1, std::min<uint64_t>(e->first_off + 1, e->prm.max_len));
-    {
-        // Queue lanes, created with the queue (an engine that never sees a single-buffer call holds
-        // no lane streams): each lane's passes are a long serial SHA-256 chain on a few CUs, so
-        // lanes must run side by side.  Streams beyond GPU_MAX_HW_QUEUES share hardware queues, and
-        // two lanes on one queue run their passes one after the other (the bench's process, where
-        // torch's streams came first: lanes on queues 3,4,4,3, 1.6 instead of 2.9 GiB/s at 8
-        // callers, profiles/r05/queue/).  A stream with a CU mask gets a hardware queue of its own;
-        // the mask is every CU.
-        if (hipSetDevice(e->prm.device) != hipSuccess) return false;
-        std::vector<uint32_t> mask((e->num_cus + 31) / 32, 0xFFFFFFFFu);
-        for (auto& q : e->qs)
-            if (!q && hipExtStreamCreateWithCUMask(&q, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
-                q = nullptr;
-                e->q_state = -1;  // the direct path serves every call
-                return false;
-            }
-    }
-    e->qb.reset(new QueueBackend{e, slot, 1024, slot / 2, slot / shortest + 2ull * 1024});
     CoalescingQueue<QueueBackend>::Config c;
     c.lanes = kQueueLanes;
 #ifdef SDFS_TUNING
@@ -1181,6 +1163,25 @@ bool queue_ready(DevEngine* e) {
     c.nslots = c.lanes + kQueueSpareSlots;
     c.max_reqs = 1024;
     c.max_req_bytes = slot / 2;
+    {
+        // Queue lanes, created with the queue (an engine that never sees a single-buffer call holds
+        // no lane streams): each lane's passes are a long serial SHA-256 chain on a few CUs, so
+        // lanes must run side by side.  Streams beyond GPU_MAX_HW_QUEUES share hardware queues, and
+        // two lanes on one queue run their passes one after the other (the bench's process, where
+        // torch's streams came first: lanes on queues 3,4,4,3, 1.6 instead of 2.9 GiB/s at 8
+        // callers, profiles/r05/queue/).  A stream with a CU mask gets a hardware queue of its own;
+        // the mask is every CU.  (Such a stream synchronises with the legacy null stream, which the
+        // engine never uses.)
+        if (hipSetDevice(e->prm.device) != hipSuccess) return false;
+        std::vector<uint32_t> mask((e->num_cus + 31) / 32, 0xFFFFFFFFu);
+        for (int l = 0; l < c.lanes; l++)
+            if (!e->qs[l] && hipExtStreamCreateWithCUMask(&e->qs[l], (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+                e->qs[l] = nullptr;
+                e->q_state = -1;  // the direct path serves every call
+                return false;
+            }
+    }
+    e->qb.reset(new QueueBackend{e, slot, 1024, slot / 2, slot / shortest + 2ull * 1024});
     e->q.reset(new CoalescingQueue<QueueBackend>(*e->qb, c));
     if (e->q->start() != 0) {  // pinned/device allocation failed: the direct path serves every call
         e->q.reset();
@@ -1190,7 +1191,7 @@ bool queue_ready(DevEngine* e) {
     }
     // first work on a stream sets up its hardware queue (milliseconds): do it for every lane now
     for (hipStream_t st : e->qs)
-        if (hipMemsetAsync(e->zero_page.p, 0, 256, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        if (st && (hipMemsetAsync(e->zero_page.p, 0, 256, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess))
             (void)hipGetLastError();
     e->q_state = 1;
     return true;

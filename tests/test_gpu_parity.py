@@ -130,6 +130,32 @@ def test_ragged_batch_vs_oracle():
             assert_same((st[b, :c], ln[b, :c], dg[b, :c]), exp, (b, prm))
 
 
+def test_small_batch_walk_routes_at_the_lds_limit():
+    """Small batches resolve their cuts from LDS (cdc_resolve_small_kernel: a buffer's whole bitmap,
+    up to 512 KiB = 16 Ki words); a batch whose longest buffer is past that takes the global walk.
+    Both sides of the limit, ragged (empty, 64 B, exactly 512 KiB, one byte over) and uniform
+    device-resident 512 KiB buffers, single queue calls of exactly 512 KiB, all vs the oracle."""
+    lim = 32 * 16384
+    for lens in ([lim, 0, 64, 300001, lim - 1, 4096], [lim + 1, 0, 64, lim, 77777]):
+        lens = np.array(lens, dtype=np.uint32)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+        base = O.synth(SYNTH_SEED, 44, 0, int(offs[-1] + lens[-1]))
+        for prm in (P(), P(min_len=2047, pred_mask=0x7FF)):
+            counts, st, ln, dg = engine_for(prm).chunk_batch(base, offs, lens)
+            for b in range(len(lens)):
+                buf = base[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+                exp = O.chunk(buf, O.Params(**prm)) if lens[b] else ([], [], [])
+                assert_same((st[b, :counts[b]], ln[b, :counts[b]], dg[b, :counts[b]]), exp, (b, int(lens[b])))
+    e = engine_for(P(min_len=2047, pred_mask=0x7FF))
+    one = O.synth(SYNTH_SEED, 45, 0, lim).tobytes()
+    assert_same(e.chunk_arrays(one), O.chunk(one, O.Params(**P(min_len=2047, pred_mask=0x7FF))), "queue call")
+    batch = DeviceBatch(e, nbuf=6, buf_len=lim)
+    batch.fill_streams(first_stream=46, bufs_per_stream=2)
+    batch.run()
+    counts, st, ln, dg, _ = batch.host_results()
+    _check_batch_against_oracle(batch, counts, st, ln, dg, P(min_len=2047, pred_mask=0x7FF), 2, 46, None)
+
+
 def test_concurrent_callers_share_one_engine():
     """SparseDedupFile.eng is one static engine used by every flush thread (SparseDedupFile.java:100)."""
     e = engine_for(P())
