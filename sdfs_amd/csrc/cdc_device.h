@@ -1804,23 +1804,196 @@ __global__ __launch_bounds__(128) void chunk_hash_split_kernel(HashArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// 5b'. packed latency form: the consumer wave runs each chunk's rounds on TWO lanes.  A lone wave
+//     issues one instruction per ~5 cycles whatever the instruction, so a chunk's chain costs its
+//     instruction count; the round's two halves are the same instructions on different data:
+//       even lane ("A")  holds a, b, c, d      odd lane ("E")  holds e, f, g, h
+//       Sigma0(a) / Sigma1(e): three v_alignbit with per-lane rotation counts + one xor3
+//       Maj(a,b,c) = (a^c) ? b : c  /  Ch(e,f,g) = e ? f : g: one bit-select after one v_bitop3
+//       T = Sigma + Maj/Ch + H with H = 0 on A, h + W[t] + K[t] on E:  A gets T2, E gets T1
+//       a' = T1 + T2 on A, e' = d + T1 on E: ONE v_add_u32 with DPP quad_perm [1,0,3,2] on
+//       Z = (E ? T : d), i.e. each lane adds its partner's Z to its own T
+//     11 instructions per round instead of 14 (the single-lane round), the state rotation is
+//     register renaming on both halves.  32 chunks per group: wave 0 builds W[t] + K[t] for them
+//     (lanes 0..31) into the odd slots of the LDS rows, whose even slots stay zero (the A lanes'
+//     W + K), wave 1 runs the rounds.  Same digests as hash_split_group.
+// ------------------------------------------------------------------------------------------
+constexpr int kSplitTasksPacked = 32;
+
+// the partner lane's value: DPP quad_perm [1,0,3,2] (lanes 2k and 2k+1 exchange)
+__device__ __forceinline__ uint32_t pair_swap(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);
+}
+
+template <int ALGO>
+__device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint32_t base, uint32_t ntask,
+                                                        uint32_t wave, uint4 (&wk)[2][16][64]) {
+    static_assert(ALGO != 2, "MD5 has no split form");
+    const uint32_t lane = threadIdx.x & 63;
+    const bool producer = wave == 0, consumer = wave == 1;
+    // the producer's lane k and the consumer's lanes 2k, 2k+1 hold chunk base + k
+    const uint32_t k = producer ? lane : lane >> 1;
+    const uint32_t i = base + k;
+    const bool valid = k < (uint32_t)kSplitTasksPacked && i < ntask;
+    uint32_t slot = 0, b = 0, kk = 0, cs = 0, len = 0, nfull = 0, nblocks = 0;
+    const uint8_t* p = a.zero_page;
+    if (valid) {
+        slot = a.tasks[i];
+        b = slot / a.cap;
+        kk = slot - b * a.cap;
+        const uint64_t boff = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
+        cs = a.starts[slot];
+        len = a.clens[slot];
+        p = a.data + boff + cs;
+        nfull = len >> 6;
+        nblocks = (len + 8) / 64 + 1;
+    }
+    const uint32_t maxnb = wave_max_u32(nblocks);  // identical in both waves (same 32 tasks)
+    if (producer) {
+        // the A lanes' W + K: zero, once for both buffers
+#pragma unroll
+        for (int g = 0; g < 16; g++) {
+            if (lane < 32) {
+                wk[0][g][2 * lane] = make_uint4(0, 0, 0, 0);
+                wk[1][g][2 * lane] = make_uint4(0, 0, 0, 0);
+            }
+        }
+    }
+    // consumer lane constants: rotation counts, the Maj/Ch mask, the H mask, the E-lane mask
+    const bool elane = (lane & 1) != 0;
+    const uint32_t R1 = elane ? 6u : 2u, R2 = elane ? 11u : 13u, R3 = elane ? 25u : 22u;
+    const uint32_t MA = elane ? 0u : ~0u;
+    const uint32_t ME = ~MA;
+    uint32_t x0 = elane ? 0x510e527fu : 0x6a09e667u, x1 = elane ? 0x9b05688cu : 0xbb67ae85u,
+             x2 = elane ? 0x1f83d9abu : 0x3c6ef372u, x3 = elane ? 0x5be0cd19u : 0xa54ff53au;
+    uint4 nx[4];
+    if (producer) load_block64(nx, nfull ? p : a.zero_page);
+    for (uint32_t it = 0; it <= maxnb; it++) {
+        if (producer) {
+            if (it < maxnb) {
+                const uint32_t blk = it;
+                uint4 cur[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) cur[q] = nx[q];
+                load_block64(nx, blk + 1 < nfull ? p + 64 * (blk + 1) : a.zero_page);
+                if (valid && blk < nblocks) {
+                    uint32_t w[16];
+                    if (blk < nfull) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            w[4 * q] = __builtin_bswap32(cur[q].x);
+                            w[4 * q + 1] = __builtin_bswap32(cur[q].y);
+                            w[4 * q + 2] = __builtin_bswap32(cur[q].z);
+                            w[4 * q + 3] = __builtin_bswap32(cur[q].w);
+                        }
+                    } else {
+                        if (blk == nfull) {
+                            tail_words<true>(w, p + 64 * nfull, len & 63);
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 16; j++) w[j] = 0;
+                        }
+                        if (blk == nblocks - 1) {
+                            const uint64_t bits = (uint64_t)len * 8;
+                            w[14] = (uint32_t)(bits >> 32);
+                            w[15] = (uint32_t)bits;
+                        }
+                    }
+                    uint4(*dst)[64] = wk[blk & 1];
+#pragma unroll
+                    for (int g = 0; g < 16; g++) {
+                        if (g >= 4 && (g & 3) == 0) {
+#pragma unroll
+                            for (int j = 0; j < 16; j++) {
+                                const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+                                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                                w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+                            }
+                        }
+                        const int t = 4 * g;
+                        dst[g][2 * lane + 1] = make_uint4(w[t & 15] + kSha256K[t], w[(t + 1) & 15] + kSha256K[t + 1],
+                                                          w[(t + 2) & 15] + kSha256K[t + 2],
+                                                          w[(t + 3) & 15] + kSha256K[t + 3]);
+                    }
+                }
+            }
+        } else if (consumer && it >= 1) {
+            const uint32_t blk = it - 1;
+            if (valid && blk < nblocks) {  // the same for both lanes of a chunk
+                const uint4(*src)[64] = wk[blk & 1];
+                const uint32_t s0 = x0, s1 = x1, s2 = x2, s3 = x3;
+                uint4 q = src[0][lane];
+                uint32_t H = (x3 & ME) + q.x;
+#pragma unroll
+                for (int g = 0; g < 16; g++) {
+                    const uint4 qn = g < 15 ? src[g + 1][lane] : make_uint4(0, 0, 0, 0);
+                    const uint32_t wkv[5] = {q.x, q.y, q.z, q.w, qn.x};
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t S = xor3(__builtin_amdgcn_alignbit(x0, x0, R1), __builtin_amdgcn_alignbit(x0, x0, R2),
+                                                __builtin_amdgcn_alignbit(x0, x0, R3));
+                        const uint32_t Y = __builtin_amdgcn_bitop3_b32(x0, x2, MA, 0x78);   // x0 ^ (x2 & MA)
+                        const uint32_t CM = __builtin_amdgcn_bitop3_b32(Y, x1, x2, 0xCA);  // Y ? x1 : x2
+                        const uint32_t T = S + CM + H;
+                        const uint32_t Z = elane ? T : x3;
+                        // next round's H from the next round's h (x2 now), then the partner add
+                        H = (x2 & ME) + wkv[r + 1];
+                        const uint32_t N = pair_swap(Z) + T;
+                        x3 = x2;
+                        x2 = x1;
+                        x1 = x0;
+                        x0 = N;
+                    }
+                    q = qn;
+                }
+                x0 += s0;
+                x1 += s1;
+                x2 += s2;
+                x3 += s3;
+            }
+        }
+        __syncthreads();
+    }
+    // e..h from the E lane, stored by the A lane
+    const uint32_t e4 = pair_swap(x0), e5 = pair_swap(x1), e6 = pair_swap(x2), e7 = pair_swap(x3);
+    if (consumer && valid && !elane) {
+        const uint32_t s[8] = {x0, x1, x2, x3, e4, e5, e6, e7};
+        store_digest<ALGO>(a, slot, b, kk, cs, len, s);
+    }
+}
+
+template <int ALGO>
+__global__ __launch_bounds__(128) void chunk_hash_split_packed_kernel(HashArgs a) {
+    __shared__ uint4 wk[2][16][64];  // [buffer][t / 4][consumer lane]: odd = W[t..t+3] + K[t..t+3], even = 0
+    const uint32_t ntask = *a.total;
+    if (blockIdx.x * kSplitTasksPacked >= ntask) return;  // whole workgroup past the end (uniform)
+    hash_split_group_packed<ALGO>(a, blockIdx.x * kSplitTasksPacked, ntask, threadIdx.x >> 6, wk);
+}
+
+// ------------------------------------------------------------------------------------------
 // 5c. throughput form with the longest chunks in the latency form (backup profile: maxLen
 //     128 KiB).  A chunk's SHA-256 is one serial chain, so a batch's longest chunk sets a floor
 //     under chunk_hash_kernel (a 55 KB chunk: 869 blocks x ~2.8 us with the GPU otherwise idle at
 //     the end, 3.50 vs 3.03 ms per 4 GiB with every chunk clipped to 32 KiB,
 //     scripts/backup_tail_probe.py).  Tasks 0 .. *nlong-1 (the chunks of more than kLongBlocks
-//     blocks, at the head of the longest-first list) go to the first workgroups in 64-chunk
-//     producer/consumer groups (section 5b: ~905 instead of ~1 423 instructions per block on the
-//     chain); the rest run one lane per chunk as in chunk_hash_kernel.
+//     blocks, at the head of the longest-first list) go to the first workgroups in producer/
+//     consumer groups: PACKED (production) the two-lane form of section 5b' (32 chunks per group,
+//     ~710 instructions per block on the chain), else the one-lane form of 5b (64 chunks, ~905);
+//     the rest run one lane per chunk as in chunk_hash_kernel.
 // ------------------------------------------------------------------------------------------
-template <int ALGO>
+template <int ALGO, bool PACKED = true>
 __global__ __launch_bounds__(256) void chunk_hash_long_kernel(HashArgs a) {
-    __shared__ uint4 wk[2][16][kSplitTasks];
+    __shared__ uint4 wk[2][16][64];
+    constexpr uint32_t G = PACKED ? kSplitTasksPacked : kSplitTasks;
     uint32_t nl = __builtin_amdgcn_readfirstlane(*a.nlong);
     if (nl > kLongSplitMax) nl = 0;
-    const uint32_t lg = (nl + kSplitTasks - 1) / kSplitTasks;  // long-chunk workgroups
+    const uint32_t lg = (nl + G - 1) / G;  // long-chunk workgroups
     if (blockIdx.x < lg) {
-        hash_split_group<ALGO>(a, blockIdx.x * kSplitTasks, nl, threadIdx.x >> 6, wk);
+        if constexpr (PACKED)
+            hash_split_group_packed<ALGO>(a, blockIdx.x * G, nl, threadIdx.x >> 6, wk);
+        else
+            hash_split_group<ALGO>(a, blockIdx.x * G, nl, threadIdx.x >> 6, wk);
         return;
     }
     const uint32_t i = nl + (blockIdx.x - lg) * 256 + threadIdx.x;

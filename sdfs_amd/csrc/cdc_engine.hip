@@ -268,6 +268,8 @@ struct DevEngine {
     // Measurement probe (tuning: SDFS_FUSED_PROBE): the batch's fingerprint kernel is replaced by
     // the fused scan + fingerprint kernel over the batch's own scan (again) and its tasks.
     int fused_probe = 0;  // form (cdc_sweep_r3.hip launch_fused_probe)
+    // latency form of the fingerprint: two lanes per chunk (tuning: SDFS_SPLIT_PACKED=0 = one lane)
+    bool split_packed = true;
     hipEvent_t ev_front = nullptr;
     ScanVariantInfo scan_info{};
     bool pred_div = false;  // divisor detector evaluated as such (scan predicate kind 3)
@@ -669,14 +671,14 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
         // chunk's serial chain: the two-wave latency form shortens it
         if (e->hash_split && e->prm.hash_algo != SDFS_CDC_MD5 && e->hash_variant == 0 &&
             max_tasks <= (uint64_t)e->num_cus * 128)
-            HIP_TRY(launch_hash_split(ha, max_tasks, s));
+            HIP_TRY(launch_hash_split(ha, max_tasks, s, e->split_packed));
 #ifdef SDFS_TUNING
         else if (e->fused_probe && fused && nbuf >= (uint32_t)e->num_cus * 4)
             HIP_TRY(launch_fused_probe(sa, ha, w->small.p + 2 * kMaxBins + 4, (int)e->prm.window, pk, e->num_cus,
                                        e->fused_probe, s));
 #endif
         else
-            HIP_TRY(launch_hash(ha, max_tasks, e->hash_variant, s));
+            HIP_TRY(launch_hash(ha, max_tasks, e->hash_variant, s, e->split_packed));
         t_end(e, t, s);
     }
     t_end(e, tpipe, s);
@@ -1280,6 +1282,7 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     }
     if (const char* v = getenv("SDFS_FRONT_SERIAL")) e->front_serial = atoi(v) != 0;
     if (const char* v = getenv("SDFS_FUSED_PROBE")) e->fused_probe = atoi(v);
+    if (const char* v = getenv("SDFS_SPLIT_PACKED")) e->split_packed = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif

@@ -202,9 +202,9 @@ hipError_t launch_scan(const ScanArgs& a, int window, int pk, int variant, int g
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);
-hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream);
+hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream, bool packed = true);
 // latency form for small batches (SHA-256 / SHA-256/160 only): two waves per 64 chunks
-hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t stream);
+hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t stream, bool packed = true);
 hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t stream);
 hipError_t launch_copy_out(const void* src, void* dst, uint64_t bytes, hipStream_t stream);
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,

@@ -829,7 +829,18 @@ hipError_t launch_scatter(const ScatterArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t s) {
+hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t s, bool packed) {
+    if (packed) {
+        // production: two lanes per chunk on the chain (11 instead of 14 instructions per round)
+        const uint32_t blocks = (uint32_t)((max_tasks + kSplitTasksPacked - 1) / kSplitTasksPacked);
+        if (blocks == 0) return hipSuccess;
+        switch (a.algo) {
+        case 0: hipLaunchKernelGGL((chunk_hash_split_packed_kernel<0>), dim3(blocks), dim3(128), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((chunk_hash_split_packed_kernel<1>), dim3(blocks), dim3(128), 0, s, a); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     const uint32_t blocks = (uint32_t)((max_tasks + kSplitTasks - 1) / kSplitTasks);
     if (blocks == 0) return hipSuccess;
     switch (a.algo) {
@@ -840,7 +851,7 @@ hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t 
     return hipGetLastError();
 }
 
-hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t s) {
+hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t s, bool packed) {
     const uint32_t blocks = (uint32_t)((max_tasks + 255) / 256);
     if (blocks == 0) return hipSuccess;
     if (variant != 0) {
@@ -852,12 +863,19 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
     }
     if (a.nlong && a.algo != 2) {
         // long chunks possible (maxLen above 32 KiB): they take the latency form (chunk_hash_long_kernel)
-        const uint32_t lg = (uint32_t)(((uint64_t)std::min<uint64_t>(a.max_long, kLongSplitMax) + kSplitTasks - 1) /
-                                       kSplitTasks);
-        if (a.algo == 0)
-            hipLaunchKernelGGL((chunk_hash_long_kernel<0>), dim3(blocks + lg), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((chunk_hash_long_kernel<1>), dim3(blocks + lg), dim3(256), 0, s, a);
+        const uint64_t g = packed ? kSplitTasksPacked : kSplitTasks;
+        const uint32_t lg = (uint32_t)(((uint64_t)std::min<uint64_t>(a.max_long, kLongSplitMax) + g - 1) / g);
+        if (packed) {
+            if (a.algo == 0)
+                hipLaunchKernelGGL((chunk_hash_long_kernel<0, true>), dim3(blocks + lg), dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL((chunk_hash_long_kernel<1, true>), dim3(blocks + lg), dim3(256), 0, s, a);
+        } else {
+            if (a.algo == 0)
+                hipLaunchKernelGGL((chunk_hash_long_kernel<0, false>), dim3(blocks + lg), dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL((chunk_hash_long_kernel<1, false>), dim3(blocks + lg), dim3(256), 0, s, a);
+        }
         return hipGetLastError();
     }
     // production: next-block prefetch issued unconditionally (ABL bit 16; interleaved A/B 2.762 ->
