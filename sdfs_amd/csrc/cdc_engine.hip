@@ -250,6 +250,7 @@ struct DevEngine {
     uint32_t scan_max_block = kScanThreads;  // widest scan workgroup (tuning build: SDFS_SCAN_MAX_BLOCK)
     bool hash_split = true;                  // latency form of the fingerprint for small batches (tuning: SDFS_HASH_SPLIT)
     bool small_seg = true;                   // short scan segments for small batches (tuning: SDFS_SMALL_SEG)
+    uint32_t small_seg_len = kSmallBatchSeg;  // their length (tuning: SDFS_SMALL_SEG_LEN, a multiple of 256)
     bool long_split = true;                  // latency form for chunks > 32 KiB (tuning: SDFS_LONG_SPLIT)
     bool par_stitch = true;                  // parallel join/place of long buffers' sections (tuning: SDFS_PAR_STITCH)
     uint32_t sec_log2 = 18;                  // section length of long buffers' cut walk (tuning: SDFS_SEC_LOG2)
@@ -463,9 +464,15 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     // 512-byte segments plus the separate walk take ~0.07 ms.  Counted in
     // segments, not buffers: 102 backup buffers of 40 MiB are a million segments.
     const uint64_t full_segs = data_bytes / e->seg_len;
-    const uint32_t seg_len = (full_segs < (uint64_t)e->num_cus * 4 * 64 && e->seg_len > kSmallBatchSeg &&
-                              e->seg_len % kSmallBatchSeg == 0 && e->small_seg)
-                                 ? kSmallBatchSeg
+    // Below 32 MiB (a queue pass: its slot is 32 MiB) the segments are halved again: the window
+    // warm-up grows from 9 to 19 % of a lane's bytes, and a lone buffer's scan (one serial LDS
+    // chain per lane) drops from 34 to 23 us (profiles/r05/small_seg/).
+    uint32_t small_len = e->small_seg_len;
+    if (full_segs < (uint64_t)e->num_cus * 4 * 8 && small_len > kTinyBatchSeg && small_len % kTinyBatchSeg == 0)
+        small_len = kTinyBatchSeg;
+    const uint32_t seg_len = (full_segs < (uint64_t)e->num_cus * 4 * 64 && e->seg_len > small_len &&
+                              e->seg_len % small_len == 0 && e->small_seg)
+                                 ? small_len
                                  : e->seg_len;
     uint32_t* hist = w->small.p;
     uint32_t* cursor = w->small.p + kMaxBins;
@@ -1264,6 +1271,10 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_HASH_SPLIT")) e->hash_split = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SMALL_SEG")) e->small_seg = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SMALL_SEG_LEN")) {
+        const uint32_t n = (uint32_t)atoi(v);
+        if (n >= 256 && n % 256 == 0) e->small_seg_len = n;
+    }
     if (const char* v = getenv("SDFS_LONG_SPLIT")) e->long_split = atoi(v) != 0;
     if (const char* v = getenv("SDFS_PAR_STITCH")) e->par_stitch = atoi(v) != 0;
     if (const char* v = getenv("SDFS_PIECE_WALK")) e->piece_walk = atoi(v) != 0;

@@ -16,6 +16,7 @@ constexpr int scan_lds_bytes(int copies) { return 2 * 256 * copies * 8; }
 
 constexpr int kScanThreads = 1024;  // widest scan workgroup (one per CU: the tables fill 128 KiB of LDS)
 constexpr uint32_t kSmallBatchSeg = 512;  // scan segment of batches with fewer buffers than SIMDs
+constexpr uint32_t kTinyBatchSeg = 256;   // ... and of batches under 32 MiB (the queue's passes)
 
 struct ScanVariantInfo {
     int copies;      // table copies (image layout)
