@@ -1103,8 +1103,18 @@ struct QueueBackend {
         }
         if (s.lo) HIP_TRY(hipMemcpyAsync(d->data.p, s.in, s.lo, hipMemcpyHostToDevice, st));
         if (s.hi < s.cap) HIP_TRY(hipMemcpyAsync(d->data.p + s.hi, s.in + s.hi, s.cap - s.hi, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(d->meta64.p, m64, 16ull * max_reqs, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(d->meta32.p, m32, 8ull * max_reqs, hipMemcpyHostToDevice, st));
+        // offsets/lengths only where a kernel reads them: the chunk requests' of a ragged pass (a
+        // uniform pass of CHUNK_LENGTH buffers, the common case, needs none) and the getHash
+        // extents' (two small copies instead of two 24 KiB ones on every pass)
+        const bool uniform_pass = s.uniform_len && (s.uniform_len & 63) == 0;
+        if (n && !uniform_pass) {
+            HIP_TRY(hipMemcpyAsync(d->meta64.p, m64, 8ull * n, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(d->meta32.p, m32, 4ull * n, hipMemcpyHostToDevice, st));
+        }
+        if (nh) {
+            HIP_TRY(hipMemcpyAsync(d->meta64.p + max_reqs, m64 + max_reqs, 8ull * nh, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(d->meta32.p + max_reqs, m32 + max_reqs, 4ull * nh, hipMemcpyHostToDevice, st));
+        }
         uint32_t* dc = reinterpret_cast<uint32_t*>(d->dimg.p);
         uint32_t* dflag = dc + n + 2 * nout;
         if (n) {
@@ -1117,7 +1127,7 @@ struct QueueBackend {
             out.total = d->total.p;
             // every CHUNK_LENGTH flush buffer (the common case) takes the uniform layout and the
             // fused cut walk; mixed lengths (write-accelerator runs) the ragged one
-            const uint32_t ul = (s.uniform_len && (s.uniform_len & 63) == 0) ? s.uniform_len : 0;
+            const uint32_t ul = uniform_pass ? s.uniform_len : 0;
             rc = device_run(e, d->data.p, s.lo, ul ? nullptr : d->meta64.p, ul ? nullptr : d->meta32.p, n, ul, 0,
                             &out, st, s.max_chunk_len, nullptr, &d->ws, dflag);
             if (rc) return rc;
