@@ -481,8 +481,7 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     if (front && e->front_recorded) HIP_TRY(hipStreamWaitEvent(s, e->ev_front, 0));
     {
         const int t = t_begin(e, K_PREP, s);
-        HIP_TRY(hipMemsetAsync(w->small.p, 0, (kSmall + 8) * sizeof(uint32_t), s));
-        if (ovf_to) HIP_TRY(hipMemsetAsync(ovf_to, 0, sizeof(uint32_t), s));
+        HIP_TRY(launch_prep_zero(w->small.p, kSmall + 8, ovf_to, s));
         if (!uniform_len) HIP_TRY(launch_seg_prefix(d_lens, nbuf, seg_len, w->seg_prefix.p, s));
         t_end(e, t, s);
     }
@@ -612,11 +611,6 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     pa.rec_base = w->rec_base.p;
     pa.total = total;
     pa.grand_total = out->total;
-    {
-        const int t = t_begin(e, K_PREFIX, s);
-        HIP_TRY(launch_prefix(pa, s));
-        t_end(e, t, s);
-    }
     ScatterArgs ca{};
     ca.counts = out->counts;
     ca.clens = out->lens;
@@ -626,7 +620,17 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     ca.nbins = e->nbins;
     ca.cursor = cursor;
     ca.tasks = w->tasks.p;
-    {
+    if ((uint64_t)nbuf * out->cap <= kSmallScatterSlots && e->nbins <= 1024) {
+        // a small batch (a queue pass): both in one workgroup, timed as the prefix stage
+        const int t = t_begin(e, K_PREFIX, s);
+        HIP_TRY(launch_prefix_scatter_small(pa, ca, s));
+        t_end(e, t, s);
+    } else {
+        {
+            const int t = t_begin(e, K_PREFIX, s);
+            HIP_TRY(launch_prefix(pa, s));
+            t_end(e, t, s);
+        }
         const int t = t_begin(e, K_SCATTER, s);
         HIP_TRY(launch_scatter(ca, s));
         t_end(e, t, s);

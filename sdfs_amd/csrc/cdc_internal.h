@@ -208,6 +208,9 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
 hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t stream, bool packed = true);
 hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t stream);
 hipError_t launch_copy_out(const void* src, void* dst, uint64_t bytes, hipStream_t stream);
+hipError_t launch_prep_zero(uint32_t* small, uint32_t words, uint32_t* flag, hipStream_t stream);
+constexpr uint64_t kSmallScatterSlots = 65536;  // chunk slots up to which prefix + scatter run fused
+hipError_t launch_prefix_scatter_small(const PrefixArgs& a, const ScatterArgs& c, hipStream_t stream);
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t stream_id, uint64_t offset,
                         hipStream_t stream);
 bool scan_window_supported(int window);

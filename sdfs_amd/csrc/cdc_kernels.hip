@@ -821,6 +821,67 @@ __global__ __launch_bounds__(kScatterThreads) void cdc_scatter_kernel(ScatterArg
             a.tasks[lbase[bin[k]] + loc[k]] = (uint32_t)(s0 + (uint64_t)k * kScatterThreads + threadIdx.x);
 }
 
+// Small batches (a queue pass: at most kSmallScatterSlots chunk slots): prefix and scatter in ONE
+// 1024-thread workgroup, the bin cursors in LDS (one launch instead of two on the pass's critical
+// path).  Same outputs: cursor (advanced past each bin's tasks, as the scatter leaves it), rec_base,
+// total, and the task list grouped by bin, longest first (the order inside a bin is free).
+__global__ __launch_bounds__(1024) void cdc_prefix_scatter_small_kernel(PrefixArgs a, ScatterArgs c) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t lcur[kMaxBins];
+    const uint32_t t = threadIdx.x;
+    part[t] = t < a.nbins ? a.hist[a.nbins - 1 - t] : 0;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    if (t < a.nbins) lcur[a.nbins - 1 - t] = part[t] - a.hist[a.nbins - 1 - t];
+    __syncthreads();
+    const uint32_t per = (a.nbuf + 1023) / 1024;
+    const uint32_t b0 = t * per, b1 = (b0 + per < a.nbuf) ? b0 + per : a.nbuf;
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; b++) sum += a.counts[b];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const uint32_t base = a.base_in ? *a.base_in : 0u;
+    uint32_t run = base + part[t] - sum;
+    if (a.rec_base)
+        for (uint32_t b = b0; b < b1; b++) {
+            a.rec_base[b] = run;
+            run += a.counts[b];
+        }
+    if (t == 1023) {
+        *a.total = part[1023];
+        if (a.base_out) *a.base_out = base + part[1023];
+        if (a.grand_total) *a.grand_total = base + part[1023];
+    }
+    const uint32_t nslots = c.nbuf * c.cap;
+    for (uint32_t slot = t; slot < nslots; slot += 1024) {
+        const uint32_t b = slot / c.cap, i = slot - b * c.cap;
+        if (i < c.counts[b]) {
+            uint32_t bb = sha_blocks(c.clens[slot]) >> c.bin_shift;
+            bb = bb < c.nbins ? bb : c.nbins - 1;
+            c.tasks[atomicAdd(&lcur[bb], 1u)] = slot;
+        }
+    }
+    __syncthreads();
+    if (t < a.nbins) c.cursor[t] = lcur[t];
+}
+
+hipError_t launch_prefix_scatter_small(const PrefixArgs& a, const ScatterArgs& c, hipStream_t s) {
+    if ((uint64_t)c.nbuf * c.cap > kSmallScatterSlots || a.nbins > 1024 || c.cursor != a.cursor) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cdc_prefix_scatter_small_kernel, dim3(1), dim3(1024), 0, s, a, c);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t s) {
     const uint64_t nslots = (uint64_t)a.nbuf * a.cap;
     const uint64_t per_block = (uint64_t)kScatterThreads * kScatterPer;
@@ -916,6 +977,23 @@ __global__ __launch_bounds__(256) void synth_kernel(uint8_t* out, uint64_t n, ui
             }
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// a batch's prep: its small scratch (histogram, cursors, totals) and its overflow flag zeroed in
+// one launch (two memsets were two fill kernels on the pass's critical path)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prep_zero_kernel(uint4* small16, uint32_t n16, uint32_t* flag) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) small16[i] = make_uint4(0, 0, 0, 0);
+    if (flag && blockIdx.x == 0 && threadIdx.x == 0) *flag = 0;
+}
+
+hipError_t launch_prep_zero(uint32_t* small, uint32_t words, uint32_t* flag, hipStream_t s) {
+    if ((words & 3) || (reinterpret_cast<uintptr_t>(small) & 15)) return hipErrorInvalidValue;
+    const uint32_t n16 = words / 4;
+    hipLaunchKernelGGL(prep_zero_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n16 + 255) / 256, 8))), dim3(256), 0,
+                       s, reinterpret_cast<uint4*>(small), n16, flag);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
