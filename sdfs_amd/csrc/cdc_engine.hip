@@ -271,6 +271,8 @@ struct DevEngine {
     int fused_probe = 0;  // form (cdc_sweep_r3.hip launch_fused_probe)
     // latency form of the fingerprint: two lanes per chunk (tuning: SDFS_SPLIT_PACKED=0 = one lane)
     bool split_packed = true;
+    // small-batch cut walk: candidate list + successors (tuning: SDFS_SMALL_BALLOT=1 = ballots only)
+    bool small_ballot = false;
     hipEvent_t ev_front = nullptr;
     ScanVariantInfo scan_info{};
     bool pred_div = false;  // divisor detector evaluated as such (scan predicate kind 3)
@@ -550,6 +552,7 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     ra.hist = hist;
     ra.overflow = ovf_to ? ovf_to : w->overflow();
     ra.max_buf_len = uniform_len ? uniform_len : max_buf_len;
+    ra.small_ballot = e->small_ballot ? 1u : 0u;
     ra.sec_len = sec_len;
     if (sec_len) {
         ra.nsec = nsec;
@@ -1308,6 +1311,7 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_FRONT_SERIAL")) e->front_serial = atoi(v) != 0;
     if (const char* v = getenv("SDFS_FUSED_PROBE")) e->fused_probe = atoi(v);
     if (const char* v = getenv("SDFS_SPLIT_PACKED")) e->split_packed = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SMALL_BALLOT")) e->small_ballot = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;
 #endif

@@ -72,6 +72,7 @@ struct ResolveArgs {
     uint32_t spec_from_scan;
     uint32_t* seg_sum;
     uint32_t seg_len;
+    uint32_t small_ballot;  // cdc_resolve_small_kernel: 1 = 64-word ballots only, no candidate list
 };
 constexpr uint32_t kSegSumWords = 8;  // summary u16 x 8 (4 words) | ncand | ovf_off | pad
 constexpr uint32_t kJoinExtra = 8;  // true chunk starts a section may take before its chains meet

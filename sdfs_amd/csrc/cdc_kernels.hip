@@ -305,17 +305,44 @@ __global__ __launch_bounds__(256) void cdc_resolve_lds_kernel(ResolveArgs a) {
 
 // Small batches (a coalescing-queue pass: a few CHUNK_LENGTH buffers): one workgroup per buffer
 // copies the buffer's whole candidate bitmap into LDS with every thread at once (8 KiB words for
-// 256 KiB, one round of 16-byte loads), then wave 0 walks the cuts from LDS.  The global walk of
-// cdc_resolve_kernel pays one dependent bitmap load per cut (~0.7 us: ~45 us for a 256 KiB buffer
-// at the 4 KiB mix), and a lone pass's latency is what a synchronous getChunks caller waits for.
+// 256 KiB, one round of 8-byte loads).  The global walk of cdc_resolve_kernel pays one dependent
+// bitmap load per cut (~0.7 us: ~45 us for a 256 KiB buffer at the 4 KiB mix), and a lone pass's
+// latency is what a synchronous getChunks caller waits for.  From LDS:
+//   1. the candidates in one ascending list (per-thread popcounts, a block prefix, each thread
+//      writes its words' positions) — up to kSmallListCap of them, else step 3 alone;
+//   2. every candidate's successor, in parallel: the first candidate at or past its position + 1 +
+//      first_off (binary search of the list), i.e. the cut the greedy walk takes next when no
+//      forced cut intervenes;
+//   3. wave 0 follows the successors (one LDS read per cut); a forced cut (max_len) or the tail
+//      starts the chain again from a binary search.  A buffer with more candidates than the list
+//      holds (zero runs: every position a candidate) is walked by 64-word ballots instead.
+// The cuts are the greedy loop's exactly: each one is the first candidate in
+// [start + first_off, start + max_len - 1], else the forced/tail position.
 constexpr uint32_t kSmallWalkWords = 16384;  // buffers up to 512 KiB
 constexpr uint32_t kSmallWalkMaxBufs = 1024;  // beyond: the global walk, several buffers per wave
+constexpr uint32_t kSmallListCap = 2048;      // candidates of one buffer in the list form
+
+// first index i in list[0, n) with list[i].x >= target (n if none)
+__device__ __forceinline__ uint32_t list_lower_bound(const uint2* list, uint32_t n, uint32_t target) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (list[mid].x < target)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
 
 __global__ __launch_bounds__(256) void cdc_resolve_small_kernel(ResolveArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t win[kSmallWalkWords];
+    __shared__ uint2 list[kSmallListCap];  // {position, index of its successor}
     __shared__ uint32_t lhist[kMaxBins];
+    __shared__ uint32_t scan[256];
     for (uint32_t i = threadIdx.x; i < a.nbins; i += 256) lhist[i] = 0;
     const uint32_t b = blockIdx.x;
+    const uint32_t t = threadIdx.x;
     const uint64_t off = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
     const uint32_t len = a.uniform_len ? a.uniform_len : a.lens[b];
     const uint32_t nwords = (len + 31) >> 5;
@@ -329,25 +356,66 @@ __global__ __launch_bounds__(256) void cdc_resolve_small_kernel(ResolveArgs a) {
         uint2 v[kPer];
 #pragma unroll
         for (uint32_t k = 0; k < kPer; k++) {
-            const uint32_t i = threadIdx.x + k * 256;
+            const uint32_t i = t + k * 256;
             v[k] = i < n2 ? src[i] : make_uint2(0, 0);
         }
 #pragma unroll
         for (uint32_t k = 0; k < kPer; k++) {
-            const uint32_t i = threadIdx.x + k * 256;
+            const uint32_t i = t + k * 256;
             if (i < n2) dst[i] = v[k];
         }
     }
     __syncthreads();
-    if (threadIdx.x < 64) {
-        const uint32_t lane = threadIdx.x;
-        uint32_t start = 0, cnt = 0;
+    // 1. the candidate list: thread t owns words [w0, w1); positions past len are not candidates
+    const uint32_t per = (nwords + 255) / 256;
+    const uint32_t w0 = min(t * per, nwords), w1 = min(w0 + per, nwords);
+    const uint32_t tail_mask = (len & 31) ? (1u << (len & 31)) - 1u : ~0u;
+    uint32_t mine = 0;
+    for (uint32_t w = w0; w < w1; w++) mine += __builtin_popcount(w + 1 == nwords ? win[w] & tail_mask : win[w]);
+    scan[t] = mine;
+    __syncthreads();
+    for (uint32_t o = 1; o < 256; o <<= 1) {
+        const uint32_t v = t >= o ? scan[t - o] : 0;
+        __syncthreads();
+        scan[t] += v;
+        __syncthreads();
+    }
+    const uint32_t total = scan[255];
+    const bool listed = total <= kSmallListCap && !a.small_ballot;
+    if (listed) {
+        uint32_t at = scan[t] - mine;
+        for (uint32_t w = w0; w < w1; w++) {
+            uint32_t bits = w + 1 == nwords ? win[w] & tail_mask : win[w];
+            while (bits) {
+                list[at++].x = w * 32 + __builtin_ctz(bits);
+                bits &= bits - 1;
+            }
+        }
+    }
+    __syncthreads();
+    // 2. successors
+    if (listed)
+        for (uint32_t i = t; i < total; i += 256) list[i].y = list_lower_bound(list, total, list[i].x + 1 + a.first_off);
+    __syncthreads();
+    if (t < 64) {
+        const uint32_t lane = t;
+        uint32_t start = 0, cnt = 0, my_s = 0, my_e = 0;
+        uint32_t j = listed ? list_lower_bound(list, total, a.first_off) : 0;  // first candidate >= lo
         while (start < len) {
             const uint32_t lo = start + a.first_off;
             const uint32_t forced = start + a.max_len - 1;
             const uint32_t hi = forced < len - 1 ? forced : len - 1;
             int64_t k = -1;
-            if (lo <= hi) {
+            if (listed) {
+                // list[j] is the first candidate >= lo: a cut when it is <= hi
+                if (lo <= hi && j < total) {
+                    const uint2 e = list[j];
+                    if (e.x <= hi) {
+                        k = e.x;
+                        j = e.y;  // the successor: first candidate >= k + 1 + first_off
+                    }
+                }
+            } else if (lo <= hi) {
                 // first candidate in [lo, hi]: 64 words (2048 positions) per ballot
                 const uint32_t wlo = lo >> 5, whi = hi >> 5;
                 for (uint32_t wb = wlo; wb <= whi; wb += 64) {
@@ -368,27 +436,38 @@ __global__ __launch_bounds__(256) void cdc_resolve_small_kernel(ResolveArgs a) {
                     }
                 }
             }
+            const bool at_candidate = k >= 0;
             if (k < 0) k = (int64_t)hi;  // forced cut at max_len, or the tail chunk
-            const uint32_t clen = (uint32_t)k + 1 - start;
-            if (cnt < a.cap) {
-                if (lane == 0) {
-                    const uint64_t slot = (uint64_t)b * a.cap + cnt;
-                    a.starts[slot] = start;
-                    a.clens[slot] = clen;
-                    uint32_t bin = sha_blocks(clen) >> a.bin_shift;
-                    bin = bin < a.nbins ? bin : a.nbins - 1;
-                    atomicAdd(&lhist[bin], 1u);
-                }
-            } else if (lane == 0) {
-                atomicOr(a.overflow, 1u);
-            }
+            // lane (cnt & 63) keeps this cut; every 64 cuts (and at the end) the wave records them
+            // together, so the serial loop carries no global stores or histogram atomics
+            const uint32_t held = cnt & 63;
+            my_s = lane == held ? start : my_s;
+            my_e = lane == held ? (uint32_t)k : my_e;
             cnt++;
             start = (uint32_t)k + 1;
+            if (held == 63 || start >= len) {
+                const uint32_t idx = cnt - 1 - held + lane;
+                if (lane <= held) {
+                    if (idx < a.cap) {
+                        const uint64_t slot = (uint64_t)b * a.cap + idx;
+                        const uint32_t clen = my_e + 1 - my_s;
+                        a.starts[slot] = my_s;
+                        a.clens[slot] = clen;
+                        uint32_t bin = sha_blocks(clen) >> a.bin_shift;
+                        bin = bin < a.nbins ? bin : a.nbins - 1;
+                        atomicAdd(&lhist[bin], 1u);
+                    } else {
+                        atomicOr(a.overflow, 1u);
+                    }
+                }
+            }
+            // a chain through a non-candidate cut restarts from a search
+            if (listed && !at_candidate && start < len) j = list_lower_bound(list, total, start + a.first_off);
         }
         if (lane == 0) a.counts[b] = cnt < a.cap ? cnt : a.cap;
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < a.nbins; i += 256)
+    for (uint32_t i = t; i < a.nbins; i += 256)
         if (lhist[i]) atomicAdd(&a.hist[i], lhist[i]);
 }
 

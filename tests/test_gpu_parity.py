@@ -156,6 +156,38 @@ def test_small_batch_walk_routes_at_the_lds_limit():
     _check_batch_against_oracle(batch, counts, st, ln, dg, P(min_len=2047, pred_mask=0x7FF), 2, 46, None)
 
 
+def test_small_batch_walk_list_and_ballot_forms():
+    """cdc_resolve_small_kernel walks a buffer's cuts through its LDS candidate list (successor
+    pointers) while the buffer holds at most 2048 candidates, and by 64-word ballots past that.
+    Ragged batches and single queue calls on both sides: random data, zero runs just under and
+    over the list's capacity, runs straddling forced (maxLen) cuts, all-zero and candidate-free
+    buffers, each vs the oracle."""
+    rng = np.random.default_rng(5150)
+    L = 262144
+    bufs = []
+    for run in (0, 1500, 2040, 2100, 6000, L):
+        h = rng.integers(0, 256, L, dtype=np.uint8)
+        o = int(rng.integers(0, L - run)) if run < L else 0
+        h[o:o + run] = 0
+        bufs.append(h)
+    h = rng.integers(0, 256, L, dtype=np.uint8)
+    h[70000:140000] = 0x55  # a candidate-free stretch: forced cuts, then the chain resumes
+    h[140000:141900] = 0
+    bufs.append(h)
+    bufs.append(np.full(L - 333, 0xFF, np.uint8))  # no candidate at all
+    lens = np.array([len(b) for b in bufs], dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    base = np.concatenate(bufs)
+    for prm in (P(), P(min_len=2047, pred_mask=0x7FF), P(min_len=0, pred_mask=0x3FF)):
+        e = engine_for(prm)
+        counts, st, ln, dg = e.chunk_batch(base, offs, lens)
+        for b, buf in enumerate(bufs):
+            exp = O.chunk(buf.tobytes(), O.Params(**prm))
+            assert_same((st[b, :counts[b]], ln[b, :counts[b]], dg[b, :counts[b]]), exp, (b, prm))
+        for b in (2, 3, 6):
+            assert_same(e.chunk_arrays(bufs[b].tobytes()), O.chunk(bufs[b].tobytes(), O.Params(**prm)), ("queue", b))
+
+
 def test_concurrent_callers_share_one_engine():
     """SparseDedupFile.eng is one static engine used by every flush thread (SparseDedupFile.java:100)."""
     e = engine_for(P())
