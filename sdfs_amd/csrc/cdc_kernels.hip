@@ -407,9 +407,11 @@ __global__ __launch_bounds__(256) void cdc_resolve_small_kernel(ResolveArgs a) {
             const uint32_t hi = forced < len - 1 ? forced : len - 1;
             int64_t k = -1;
             if (listed) {
-                // list[j] is the first candidate >= lo: a cut when it is <= hi
+                // list[j] is the first candidate >= lo: a cut when it is <= hi.  Position and
+                // successor in one ds_read_b64, issued before the tests (read separately, the
+                // successor costs a second LDS round trip per cut)
+                const uint2 e = list[j < kSmallListCap ? j : kSmallListCap - 1];
                 if (lo <= hi && j < total) {
-                    const uint2 e = list[j];
                     if (e.x <= hi) {
                         k = e.x;
                         j = e.y;  // the successor: first candidate >= k + 1 + first_off
