@@ -251,6 +251,8 @@ struct DevEngine {
     bool hash_split = true;                  // latency form of the fingerprint for small batches (tuning: SDFS_HASH_SPLIT)
     bool small_seg = true;                   // short scan segments for small batches (tuning: SDFS_SMALL_SEG)
     uint32_t small_seg_len = kSmallBatchSeg;  // their length (tuning: SDFS_SMALL_SEG_LEN, a multiple of 256)
+    uint32_t tiny_seg_len = kTinyBatchSeg;    // below 32 MiB (tuning: SDFS_TINY_SEG_LEN, a multiple of 64)
+    bool tiny_scan = true;  // passes < 32 MiB: 64/128-byte segments with ScanTiny (tuning: SDFS_TINY_SCAN=0 = off)
     bool long_split = true;                  // latency form for chunks > 32 KiB (tuning: SDFS_LONG_SPLIT)
     bool par_stitch = true;                  // parallel join/place of long buffers' sections (tuning: SDFS_PAR_STITCH)
     uint32_t sec_log2 = 18;                  // section length of long buffers' cut walk (tuning: SDFS_SEC_LOG2)
@@ -466,12 +468,22 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     // 512-byte segments plus the separate walk take ~0.07 ms.  Counted in
     // segments, not buffers: 102 backup buffers of 40 MiB are a million segments.
     const uint64_t full_segs = data_bytes / e->seg_len;
-    // Below 32 MiB (a queue pass: its slot is 32 MiB) the segments are halved again: the window
-    // warm-up grows from 9 to 19 % of a lane's bytes, and a lone buffer's scan (one serial LDS
-    // chain per lane) drops from 34 to 23 us (profiles/r05/small_seg/).
+    // Below 32 MiB (a queue pass: its slot is 32 MiB) the segments are shorter again: a lane alone
+    // on its SIMD waits out every byte's LDS round trip, so a lone pass's scan time is its lanes'
+    // chain length (segment + 48-byte warm-up).  256 bytes: a lone buffer 34 -> 23 us
+    // (profiles/r05/small_seg/); then halved while one wave per SIMD still has a segment per
+    // lane, down to 64 bytes, scanned by ScanTiny (64-byte blocks): a lone buffer 21.5 -> 10.4 us
+    // (profiles/r05/tiny_scan/).  Passes of 16-32 MiB keep 256 (more lanes than one wave per SIMD:
+    // the warm-up would only add work).
     uint32_t small_len = e->small_seg_len;
-    if (full_segs < (uint64_t)e->num_cus * 4 * 8 && small_len > kTinyBatchSeg && small_len % kTinyBatchSeg == 0)
-        small_len = kTinyBatchSeg;
+    if (full_segs < (uint64_t)e->num_cus * 4 * 8) {
+        uint32_t t = e->tiny_seg_len;
+        if (e->tiny_scan) {
+            const uint64_t per_lane = data_bytes / ((uint64_t)e->num_cus * 4 * 64);
+            while (t > 64 && t % 128 == 0 && t / 2 >= per_lane) t /= 2;
+        }
+        if (small_len > t && small_len % t == 0) small_len = t;
+    }
     const uint32_t seg_len = (full_segs < (uint64_t)e->num_cus * 4 * 64 && e->seg_len > small_len &&
                               e->seg_len % small_len == 0 && e->small_seg)
                                  ? small_len
@@ -597,7 +609,10 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     grid = std::max<uint64_t>(grid, 1);
     {
         const int t = t_begin(e, K_SCAN, s);
-        HIP_TRY(launch_scan(sa, (int)e->prm.window, pk, e->scan_variant, (int)grid, (int)block, s));
+        if (e->tiny_scan && e->scan_variant == 0 && seg_len < 256 && !sa.fuse_resolve)
+            HIP_TRY(launch_scan_tiny(sa, (int)e->prm.window, pk, (int)grid, (int)block, s));
+        else
+            HIP_TRY(launch_scan(sa, (int)e->prm.window, pk, e->scan_variant, (int)grid, (int)block, s));
         t_end(e, t, s);
     }
     if (!fused) {
@@ -1288,6 +1303,11 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_HASH_WG_PER_CU")) e->hash_wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_HASH_SPLIT")) e->hash_split = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SMALL_SEG")) e->small_seg = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_TINY_SCAN")) e->tiny_scan = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_TINY_SEG_LEN")) {
+        const int n = atoi(v);
+        if (n >= 64 && n % 64 == 0) e->tiny_seg_len = (uint32_t)n;
+    }
     if (const char* v = getenv("SDFS_SMALL_SEG_LEN")) {
         const uint32_t n = (uint32_t)atoi(v);
         if (n >= 256 && n % 256 == 0) e->small_seg_len = n;

@@ -201,6 +201,8 @@ hipError_t launch_seg_prefix(const uint32_t* lens, uint32_t nbuf, uint32_t seg_l
 // variants only), 3 = divisor detector fp % D == R (production variant only)
 hipError_t launch_scan(const ScanArgs& a, int window, int pk, int variant, int grid, int block,
                        hipStream_t stream);
+// the tiny-batch scan (64-byte blocks, no fused walk) for segments shorter than 256 bytes
+hipError_t launch_scan_tiny(const ScanArgs& a, int window, int pk, int grid, int block, hipStream_t stream);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t stream);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);

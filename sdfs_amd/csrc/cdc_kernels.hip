@@ -45,6 +45,14 @@ namespace sdfs {
 using ScanProd = ScanCfg<32, 1, false, 4, 16 | kAblSdwa | kAblSdwaPop | kAblMinGroup | kAblMinGroup8 | kAblPopSwap, 256,
                          2, kScanThreads, true>;
 
+// Tiny batches (a lone queue pass: a few 256 KiB buffers, segments shorter than ScanProd's
+// 256-byte block): the same byte loop over 64-byte blocks and no fused walk (the separate
+// small-batch walk resolves them).  A lane alone on its SIMD waits out the LDS round trip of every
+// byte, so a lone buffer's scan time is its lanes' chain length: 64-byte segments (+ the 48-byte
+// window warm-up) instead of 256 (ScanProd with a short segment still scans its whole block).
+using ScanTiny = ScanCfg<32, 1, false, 4, 16 | kAblSdwa | kAblSdwaPop | kAblMinGroup | kAblMinGroup8 | kAblPopSwap, 64,
+                         0, kScanThreads, true>;
+
 template <class CFG>
 constexpr ScanVariantInfo info_of() {
     return {CFG::kCopies, CFG::kChains, CFG::kLds, std::max(1, CFG::kWavesPerSimd * 256 / CFG::kThreads), CFG::kBlk,
@@ -91,6 +99,17 @@ hipError_t launch_scan(const ScanArgs& a, int window, int pk, int variant, int g
     case 32: return launch_scan_wc<32, ScanProd>(a, pk, grid, block, s);
     case 48: return launch_scan_wc<48, ScanProd>(a, pk, grid, block, s);
     case 64: return launch_scan_wc<64, ScanProd>(a, pk, grid, block, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_scan_tiny(const ScanArgs& a, int window, int pk, int grid, int block, hipStream_t s) {
+    if (a.fuse_resolve) return hipErrorInvalidValue;  // the tiny form has no fused walk
+    switch (window) {
+    case 16: return launch_scan_wc<16, ScanTiny>(a, pk, grid, block, s);
+    case 32: return launch_scan_wc<32, ScanTiny>(a, pk, grid, block, s);
+    case 48: return launch_scan_wc<48, ScanTiny>(a, pk, grid, block, s);
+    case 64: return launch_scan_wc<64, ScanTiny>(a, pk, grid, block, s);
     default: return hipErrorInvalidValue;
     }
 }
