@@ -95,6 +95,28 @@ def test_golden_fixture_bit_exact(fx):
     assert_same(got, exp, fx["name"])
 
 
+@pytest.mark.parametrize("window", [16, 32, 48, 64])
+def test_every_window_through_the_small_pass_scan(window):
+    """Every supported window through the queue's lone-pass scan (64-byte segments, ScanTiny) and a
+    ragged small batch, random and zero-run buffers, against the oracle."""
+    prm = P(window=window)
+    e = engine_for(prm)
+    rng = np.random.default_rng(window)
+    bufs = [O.synth(SYNTH_SEED, 60 + window, 0, 262144), rng.integers(0, 256, 200003, dtype=np.uint8)]
+    bufs[1][5000:9000] = 0
+    bufs[1][150000:151000] = 0
+    for buf in bufs:
+        assert_same(e.chunk_arrays(buf.tobytes()), O.chunk(buf.tobytes(), O.Params(**prm)), (window, len(buf)))
+    lens = np.array([len(b) for b in bufs] + [0, 777], dtype=np.uint32)
+    base = np.concatenate(bufs + [rng.integers(0, 256, 777, dtype=np.uint8)])
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    counts, st, ln, dg = e.chunk_batch(base, offs, lens)
+    for b in range(len(lens)):
+        buf = base[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+        exp = O.chunk(buf, O.Params(**prm)) if lens[b] else ([], [], [])
+        assert_same((st[b, :counts[b]], ln[b, :counts[b]], dg[b, :counts[b]]), exp, (window, b))
+
+
 def test_get_chunks_fingers():
     data = O.synth(SYNTH_SEED, 0, 0, 262144).tobytes()
     fingers = engine_for(P()).getChunks(data, "uuid-1")
