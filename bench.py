@@ -26,6 +26,7 @@ fingerprinting).  The one-stream rate is reported beside it (`one_stream`).
 Prints ONE JSON line on rank 0 (contract in the task statement); diagnostics go to stderr.
 """
 import argparse
+import ctypes
 import json
 import os
 import subprocess
@@ -62,8 +63,91 @@ def sha_ceiling(local: int, waves_per_simd: int = 4) -> float:
     return g.value
 
 
+_probe = None
+
+
+def probe_lib():
+    import ctypes
+
+    global _probe
+    if _probe is None:
+        _probe = ctypes.CDLL(PROBE_LIB)
+        _probe.sdfs_probe_exchange_proxy_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                            ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
+    return _probe
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def roofline_block(nbytes: int, hash_ms: float, ms_step: float, sha_blocks: int, ceiling: float,
+                   traffic, traffic_src, kernel_ms_source: str, hash_ms_live=None) -> dict:
+    """The bench line's roofline for the dominant kernel (chunk_hash).  The top level is the
+    contract's HBM roofline: algorithmic bytes per launch (the input it fingerprints) over its
+    one-stream launch duration, against the 8 TB/s HBM peak.  The kernel's real limiter is VALU
+    issue of the SHA-256 mix; `valu` reports its compressed bytes against the live issue ceiling."""
+    t_dom = hash_ms / 1e3
+    achieved = nbytes / t_dom / 1e9 if t_dom > 0 else 0.0
+    valu_gbps = sha_blocks * 64 / t_dom / 1e9 if t_dom > 0 else 0.0
+    return {
+        "bound": "hbm",
+        "limiter": "valu",
+        "kernel": "chunk_hash",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "kernel_ms": round(hash_ms, 4),
+        "kernel_ms_source": kernel_ms_source,
+        "algorithmic_bytes_per_launch": nbytes,
+        "two_stream_launch_ms": round(hash_ms_live, 4) if hash_ms_live else None,
+        "achieved_per_step": round(nbytes / (ms_step / 1e3) / 1e9, 1),
+        "frac_per_step": round(nbytes / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "valu": {
+            "ceiling_gbps": round(ceiling, 1),
+            "achieved_gbps": round(valu_gbps, 1),
+            "frac": round(valu_gbps / ceiling, 4) if ceiling > 0 else None,
+            "unit": "GB/s of 64-byte SHA-256 blocks (chunk bytes + padding blocks)",
+            "sha_blocks_per_launch": sha_blocks,
+            "ceiling_source": ("production sha256_compress, register-resident data, every CU at 4 waves/SIMD, "
+                               "timed in this process (tools/probe_kernels.hip)"),
+            "note": ("the kernel is bound by VALU issue of its SHA-256 instruction mix, not by HBM: the top-level "
+                     "frac is of the 8 TB/s HBM peak, this one of the measured issue ceiling"),
+        },
+    }
+
+
+def sha_blocks_of(torch, batch) -> int:
+    """What chunk_hash compresses per launch: every chunk's 64-byte blocks incl. its padding block(s)."""
+    valid = torch.arange(batch.cap, device=batch.lens.device)[None, :] < batch.counts[:, None]
+    lens = batch.lens.view(batch.nbuf, batch.cap).to(torch.int64)
+    return int((((lens + 8) // 64 + 1) * valid).sum().item())
+
+
+def table_digest(torch, rows) -> str:
+    """SHA-256 of a record table's bytes (compares the exchanged table across bench forms)."""
+    import hashlib
+
+    return hashlib.sha256(rows.contiguous().cpu().numpy().tobytes()).hexdigest()
+
+
+def cpu_baseline_block(args, cfg):
+    aff = len(os.sched_getaffinity(0))
+    quota = cpu_quota()
+    th = args.cpu_threads or max(1, min(16 if quota is None else int(quota), aff))
+    p_kw = dict(min_len=cfg.min_len, pred_mask=cfg.pred_mask)
+    log(f"cpu baseline: {th} threads, ~{args.cpu_secs}s sample")
+    cpu = cpu_baseline(args.cpu_secs, th, p_kw)
+    if th > 1 and args.cpu_1t_secs > 0:  # SURVEY.md §8(d): T = all cores and T = 1
+        one = cpu_baseline(args.cpu_1t_secs, 1, p_kw)
+        cpu["one_thread"] = {"value": one["value"], "sample": one["sample"]}
+    cpu["cpu_model"] = cpu_model()
+    cpu["affinity_cpus"] = aff
+    cpu["cpu_quota"] = quota
+    return cpu
 
 
 def cpu_baseline(target_secs: float, threads: int, p_kw: dict):
@@ -282,20 +366,55 @@ def main_device_set(args):
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(i + k)
-    ex.exchange(i + args.steps - 1)
+    last = i + args.steps - 1
+    ex.exchange(last)
     sync_all()
     elapsed = time.perf_counter() - t0
-    hash_ms = [eng.kernel_times(d).get("chunk_hash", 0.0) for d in range(n)]
+    hash_ms_live = [eng.kernel_times(d).get("chunk_hash", 0.0) for d in range(n)]
     eng.set_timing(0)
-    totals = [int(batches[d][0].total.item()) for d in range(n)]
-    counts, stride = ex.results[-1]
     value = n * nbytes * args.steps / elapsed / 2**30
     ms_step = elapsed / args.steps * 1e3
-    t_dom = hash_ms[0] / 1e3
-    achieved = nbytes / t_dom / 1e9 if t_dom > 0 else 0.0
+
+    # the exchanged table of the last timed step, checked: every device's count is its batch's
+    # total, and device j's rows in GPU 0's gathered table are device j's own records
+    counts, stride = ex.results[-1]
+    k_last = last % ex.nslots
+    totals = [int(batches[d][last % 2].total.item()) for d in range(n)]
+    g0 = ex.gathered[0][last % 2]
+    rows_match = all(
+        torch.equal(g0[j * stride: j * stride + counts[j]].cpu(), ex.slots[j][k_last][: counts[j]].cpu())
+        for j in range(n))
+    table_sha = [table_digest(torch, ex.slots[j][k_last][: counts[j]]) for j in range(n)]
+
+    # The roofline's launch duration, per GPU: chunk_hash timed with HIP events over a one-stream
+    # region (stream-ordered, so nothing overlaps the kernel; the two-stream region's launches are
+    # stretched by the other batch's scan and are reported beside it only)
+    def one_all():
+        for d in range(n):
+            batches[d][0].run(buffer_id_base=d * batches[d][0].nbuf, stream=streams[d][0].cuda_stream)
+
+    for _ in range(2):
+        one_all()
+    sync_all()
+    eng.set_timing_stages(args.steps, ("chunk_hash",))
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        one_all()
+    sync_all()
+    el_one = time.perf_counter() - t1
+    hash_ms = [eng.kernel_times(d).get("chunk_hash", 0.0) for d in range(n)]
+    eng.set_timing(0)
+    with torch.cuda.device(0):
+        ceiling = sha_ceiling(0)  # right after the one-stream region: the same clock regime
+        sha_blocks = sha_blocks_of(torch, batches[0][0])
     params = (f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
               f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen {args.hash_type}")
     traffic, traffic_src = load_traffic("chunk_hash", params)
+    roof = roofline_block(nbytes, hash_ms[0], ms_step, sha_blocks, ceiling, traffic, traffic_src,
+                          "HIP events around chunk_hash on GPU 0's launch stream over a one-stream region of "
+                          f"{args.steps} steps per GPU (stream-ordered: nothing overlaps the kernel)",
+                          hash_ms_live[0])
+    cpu = cpu_baseline_block(args, cfg) if args.cpu_secs > 0 else None
     res = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -318,14 +437,17 @@ def main_device_set(args):
             "streams_in_flight": 2,
             "exchange": "in-process RCCL all-gather of the 48-B fingerprint records by the engine "
                         "(sdfs_cdc_allgather_records), pipelined one step behind production",
-            "exchange_last_step": {"counts": counts, "stride": stride},
+            "exchange_last_step": {"counts": counts, "stride": stride, "counts_match": counts == totals,
+                                   "rows_match": rows_match, "table_sha256": table_sha},
             "parallelism": f"device set of {n} GPUs in one process (streams sharded per GPU)",
         },
-        "kernels_ms": {"chunk_hash_per_gpu": [round(x, 4) for x in hash_ms]},
-        "roofline": {"bound": "valu", "kernel": "chunk_hash", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "traffic_source": traffic_src},
-        "cpu_baseline": None,
+        "kernels_ms": {"chunk_hash_per_gpu": [round(x, 4) for x in hash_ms],
+                       "chunk_hash_two_stream_per_gpu": [round(x, 4) for x in hash_ms_live]},
+        "one_stream": {"streams_in_flight": 1, "value": round(n * nbytes * args.steps / el_one / 2**30, 3),
+                       "ms_per_step": round(el_one / args.steps * 1e3, 4)},
+        "roofline": roof,
+        "records_sha256": table_digest(torch, batches[0][0].record_table()),
+        "cpu_baseline": cpu,
         "commit": git_head(),
     }
     print(json.dumps(res), flush=True)
@@ -370,6 +492,13 @@ def main():
                          "(the default for N > 1 without a launcher)")
     ap.add_argument("--exchange-mode", default="direct", choices=["direct", "copy"],
                     help="direct: the engine writes records into the exchange slot; copy: snapshot copy")
+    ap.add_argument("--exchange-proxy", type=int, default=0,
+                    help="W > 1 (N = 1 only): project the W-rank exchange onto one GPU -- each step, a paced copy of "
+                         "(W-1) x this GPU's record bytes on a side stream with RCCL's footprint (--proxy-wgs "
+                         "workgroups for as long as xGMI at --proxy-gbps takes; tools/probe_kernels.hip)")
+    ap.add_argument("--proxy-wgs", type=int, default=32, help="workgroups of the exchange proxy (RCCL channels)")
+    ap.add_argument("--proxy-gbps", type=float, default=300.0, help="assumed per-GPU all-gather receive rate")
+    ap.add_argument("--proxy-record-bytes", type=int, default=48, help="bytes per exchanged record")
     args = ap.parse_args()
 
     launched = "WORLD_SIZE" in os.environ
@@ -423,9 +552,25 @@ def main():
         ex = RecordExchange(batch.recs.view(-1, 48).shape[0], device, depth=2, slots=3 if direct else 2)
         ex.direct = direct
 
+    proxy = None  # set after the warmup (--exchange-proxy): [side stream, dst, src, bytes]
+
+    def proxy_after(stream):
+        """The projected exchange of the step just issued on `stream`: the paced copy on a side
+        stream behind the step's production, as RecordExchange runs RCCL behind it."""
+        px, dst, src, nb = proxy
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        px.wait_event(ev)
+        rc = probe_lib().sdfs_probe_exchange_proxy_launch(dst.data_ptr(), src.data_ptr(), nb, args.proxy_wgs,
+                                                          ctypes.c_double(args.proxy_gbps), px.cuda_stream)
+        if rc:
+            raise RuntimeError(f"exchange proxy launch failed: {rc}")
+
     def step():
         if nsf >= 2:
             runner.step(base_id, ex)
+            if proxy is not None:
+                proxy_after(runner.streams[(runner.k - 1) % len(runner.streams)])
         else:
             rec = None
             if ex is not None and ex.direct:
@@ -434,10 +579,16 @@ def main():
             batch.run(buffer_id_base=base_id, stream=cs.cuda_stream)
             if ex is not None:
                 ex.submit(rec if rec is not None else batch.recs.view(-1, 48), batch.total, stream=cs)
+            if proxy is not None:
+                proxy_after(cs)
+
+    last_exchange = []
 
     def drain():
         if ex is not None:
-            ex.flush()
+            r = ex.flush()
+            if r:
+                last_exchange[:] = [r[-1], (ex.n - 1) % ex.nslots]
 
     # clock ramp: ~0.3 s of chunking before the W warmup steps (the GPU idles while the host sets
     # up and its clocks drop; a few 4.5 ms steps do not bring them back), outside the timed region
@@ -448,6 +599,27 @@ def main():
     for _ in range(args.warmup):
         step()
     drain()
+    proxy_info = None
+    if args.exchange_proxy > 1:
+        if world != 1:
+            raise SystemExit("--exchange-proxy projects N ranks onto one GPU: run it at N = 1")
+        torch.cuda.synchronize()
+        recs = int(batch.total.item())
+        nb = ((args.exchange_proxy - 1) * recs * args.proxy_record_bytes + 15) // 16 * 16
+        proxy = [torch.cuda.Stream(device=device), torch.empty(nb, dtype=torch.uint8, device=device),
+                 torch.zeros(nb, dtype=torch.uint8, device=device), nb]
+        # the proxy alone on the idle GPU: its own duration (the projected xGMI time)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(proxy[0])
+        proxy_after(proxy[0])
+        e1.record(proxy[0])
+        e1.synchronize()
+        proxy_info = {"ranks": args.exchange_proxy, "bytes_per_step": nb, "records_per_gpu_step": recs,
+                      "record_bytes": args.proxy_record_bytes, "workgroups": args.proxy_wgs,
+                      "gbps": args.proxy_gbps, "alone_ms": round(e0.elapsed_time(e1), 4)}
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
     # timed region: HIP events only around the dominant kernel (the roofline's launch duration)
     eng.set_timing_stages(args.steps, ("chunk_hash",))
 
@@ -473,9 +645,22 @@ def main():
     kt = eng.kernel_times()
     eng.set_timing(0)
     counts, _, _, _, total = batch.host_results()
-    # what chunk_hash compresses per launch: every chunk's 64-byte blocks incl. its padding block(s)
-    valid = torch.arange(batch.cap, device=batch.lens.device)[None, :] < batch.counts[:, None]
-    sha_blocks = int((((batch.lens.view(nbuf, batch.cap).to(torch.int64) + 8) // 64 + 1) * valid).sum().item())
+    sha_blocks = sha_blocks_of(torch, batch)
+    records_sha = table_digest(torch, batch.record_table())
+    # the exchanged table of the last timed step, checked: every rank's count, and this rank's rows
+    # of the gathered table equal the records its engine wrote
+    ex_check = None
+    if ex is not None and last_exchange:
+        (gathered, cl), k_last = last_exchange
+        mx = max(cl)
+        mine = gathered[rank * mx: rank * mx + cl[rank]]
+        tot = torch.tensor([total], device=device, dtype=torch.int64)
+        tots = [torch.zeros_like(tot) for _ in range(world)]
+        dist.all_gather(tots, tot)
+        tots = [int(x.item()) for x in tots]
+        ex_check = {"counts": cl, "stride": mx, "counts_match": cl == tots,
+                    "rows_match": bool(torch.equal(mine, ex.slots[k_last][: cl[rank]])),
+                    "table_sha256": [table_digest(torch, mine)] if rank == 0 else None}
 
     # The roofline's launch duration: chunk_hash timed with HIP events over a one-stream timed
     # region (every step stream-ordered, so no other kernel shares the GPU with chunk_hash and its
@@ -509,6 +694,13 @@ def main():
                      "ms_per_step": round(el / args.steps * 1e3, 4)}
     if world > 1:
         other = None
+        # every rank's one-stream chunk_hash launch (the roofline uses rank 0's)
+        t = torch.tensor([hash_ms_one], device=device, dtype=torch.float64)
+        per = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(per, t)
+        hash_ms_ranks = [round(float(x.item()), 4) for x in per]
+    else:
+        hash_ms_ranks = [round(hash_ms_one, 4)]
     ceiling = sha_ceiling(local)  # right after the one-stream region: the same clock regime
 
     # the other chunk mix beside the headline: the reference default (minLen 4095, 12-bit) when
@@ -592,29 +784,15 @@ def main():
         return
 
     value = world * nbytes * args.steps / elapsed / 2**30
-    t_dom = hash_ms_one / 1e3
-    achieved = nbytes / t_dom / 1e9 if t_dom > 0 else 0.0
     ms_step = elapsed / args.steps * 1e3
     # the roofline's kernel time cannot exceed the step it is part of
     assert 0 < hash_ms_one <= ms_step, f"chunk_hash {hash_ms_one:.3f} ms per launch > {ms_step:.3f} ms per step"
     params = (f"P=0x26CE86126EF863 W=48 minLen={cfg.min_len} maxLen={cfg.max_len} "
               f"pred=(fp&{cfg.pred_mask:#x})==0 n>minLen {args.hash_type}")
     traffic, traffic_src = load_traffic("chunk_hash", params)
-    cpu = None
-    if world == 1 and args.cpu_secs > 0:
-        # the GPU box's CPU share is 16 cores per GPU (the host's nproc shows the whole machine)
-        aff = len(os.sched_getaffinity(0))
-        quota = cpu_quota()
-        th = args.cpu_threads or max(1, min(16 if quota is None else int(quota), aff))
-        p_kw = dict(min_len=cfg.min_len, pred_mask=cfg.pred_mask)
-        log(f"cpu baseline: {th} threads, ~{args.cpu_secs}s sample")
-        cpu = cpu_baseline(args.cpu_secs, th, p_kw)
-        if th > 1 and args.cpu_1t_secs > 0:  # T = all cores and T = 1
-            one = cpu_baseline(args.cpu_1t_secs, 1, p_kw)
-            cpu["one_thread"] = {"value": one["value"], "sample": one["sample"]}
-        cpu["cpu_model"] = cpu_model()
-        cpu["affinity_cpus"] = aff
-        cpu["cpu_quota"] = quota
+    # the CPU restatement on rank 0's host share (the GPU box's CPU share is 16 cores per GPU;
+    # the host's nproc shows the whole machine), after all GPU work
+    cpu = cpu_baseline_block(args, cfg) if args.cpu_secs > 0 else None
     res = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -638,38 +816,19 @@ def main():
             "records_identical_across_streams": identical,
             "exchange": (f"RCCL all_gather of 48-B fingerprint records, pipelined ({args.exchange_mode})"
                          if use_ex else "none (N=1)"),
+            "exchange_last_step": ex_check,
             "parallelism": f"dp{world} (streams sharded per GPU)",
         },
         "kernels_ms": {k: round(v, 4) for k, v in kt.items()},
         "kernels_note": "every stage: HIP events around each kernel in a separate untimed one-stream pass",
-        "roofline": {
-            "bound": "valu",
-            "kernel": "chunk_hash",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "kernel_ms": round(hash_ms_one, 4),
-            "kernel_ms_source": ("HIP events around chunk_hash on its launch stream over a one-stream timed region of "
-                                 f"{args.steps} steps (stream-ordered: nothing overlaps the kernel)"),
-            "algorithmic_bytes_per_launch": nbytes,
-            "two_stream_launch_ms": round(hash_ms_live, 4) if nsf >= 2 else None,
-            "achieved_per_step": round(nbytes / (ms_step / 1e3) / 1e9, 1),
-            "frac_per_step": round(nbytes / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-            "valu": {
-                "ceiling_gbps": round(ceiling, 1),
-                "achieved_gbps": round(sha_blocks * 64 / t_dom / 1e9, 1),
-                "frac": round(sha_blocks * 64 / t_dom / 1e9 / ceiling, 4),
-                "unit": "GB/s of 64-byte SHA-256 blocks (chunk bytes + padding blocks)",
-                "sha_blocks_per_launch": sha_blocks,
-                "ceiling_source": ("production sha256_compress, register-resident data, every CU at 4 waves/SIMD, "
-                                   "timed in this process (tools/probe_kernels.hip)"),
-                "note": ("the kernel is bound by VALU issue of its SHA-256 instruction mix, not by HBM: frac above "
-                         "is of the 8 TB/s HBM peak, this one of the measured issue ceiling"),
-            },
-        },
+        "roofline": roofline_block(
+            nbytes, hash_ms_one, ms_step, sha_blocks, ceiling, traffic, traffic_src,
+            "HIP events around chunk_hash on its launch stream over a one-stream timed region of "
+            f"{args.steps} steps (stream-ordered: nothing overlaps the kernel)",
+            hash_ms_live if nsf >= 2 else None),
+        "chunk_hash_ms_per_rank": hash_ms_ranks,
+        "exchange_proxy": proxy_info,
+        "records_sha256": records_sha,
         "cpu_baseline": cpu,
         ("one_stream" if nsf >= 2 else "two_streams"): other,
         ("at_ref_default" if main_is_4k else "at_4k_mean"): other_mix,

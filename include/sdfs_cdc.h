@@ -198,6 +198,10 @@ int sdfs_cdc_get_chunks_fill(sdfs_cdc_engine* e, uint64_t stream_key, uint32_t l
  * callers' copies into pinned staging, and on the device (transfers + kernels). */
 int sdfs_cdc_queue_stats(sdfs_cdc_engine* e, uint64_t* batches, uint64_t* requests);
 int sdfs_cdc_queue_timing(sdfs_cdc_engine* e, double* fill_us, double* copy_us, double* device_us);
+/* getChunks calls answered before the rest of their GPU pass finished: a pass's callers each
+ * return once their own buffer's last chunk is fingerprinted, not when the pass's longest chunk
+ * is (SparseDedupFile.java:432 callers block on that call).  Cumulative, all devices. */
+int sdfs_cdc_queue_early(sdfs_cdc_engine* e, uint64_t* early);
 
 /* Batched getChunks over nbuf independent host buffers at base+offs[b], lens[b] (each chunked
  * from fresh state; SURVEY.md 0 "every call starts from a fresh state").  Per-buffer slots of

@@ -49,7 +49,19 @@ public final class HipVariableSha256HashEngine implements AbstractHashEngine {
         String[] f = spec.trim().split(":");
         if (f.length != 3 || !(f[0].equals("mask") || f[0].equals("div")))
             throw new IOException("sdfs.hip.boundary must be mask:M:V or div:D:R, got " + spec);
-        return new long[] {f[0].equals("div") ? 1 : 0, Long.decode(f[1]), Long.decode(f[2])};
+        return new long[] {f[0].equals("div") ? 1 : 0, unsigned(f[1], spec), unsigned(f[2], spec)};
+    }
+
+    /** A 64-bit unsigned field (decimal or 0x hex, e.g. 0xFFFFFFFFFFFFFFFF); a malformed one is an
+     *  IOException naming the property, as the constructor declares. */
+    static long unsigned(String v, String spec) throws IOException {
+        String t = v.trim();
+        try {
+            if (t.startsWith("0x") || t.startsWith("0X")) return Long.parseUnsignedLong(t.substring(2), 16);
+            return Long.parseUnsignedLong(t);
+        } catch (NumberFormatException ex) {
+            throw new IOException("sdfs.hip.boundary: bad number '" + v + "' in " + spec, ex);
+        }
     }
 
     @Override public boolean isVariableLength() { return true; }

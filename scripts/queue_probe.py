@@ -43,6 +43,7 @@ for th in [int(x) for x in os.environ.get("THREADS", "1,32,128,384").split(",")]
     e = HipVariableSha256HashEngine(config=cfg)
     T.getchunks(e, th, host, L, max(256, 4 * th), mode=MODE)  # warm: every slot and lane carries a pass
     b0 = e.queue_stats()
+    q0 = e.queue_early() if hasattr(e._lib, "sdfs_cdc_queue_early") else 0
     c0 = cpu_stat()
     calls = max(256, th * 8)
     r, _ = T.getchunks(e, th, host, L, calls, mode=MODE)
@@ -50,9 +51,12 @@ for th in [int(x) for x in os.environ.get("THREADS", "1,32,128,384").split(",")]
         raise SystemExit(f"getChunks failed at {th} threads: status {r.first_error}")
     c1 = cpu_stat()
     b1 = e.queue_stats()
+    early = (e.queue_early() - q0) if hasattr(e._lib, "sdfs_cdc_queue_early") else None
     thr = {k: c1[k] - c0.get(k, 0) for k in ("nr_throttled", "throttled_usec", "usage_usec") if k in c1}
     print(json.dumps({"threads": th, "qi": os.environ.get("SDFS_Q_INFLIGHT", "default"), "gibps": round(r.gibps, 3),
-                      "p50_us": round(r.p50_us), "p99_us": round(r.p99_us), "calls_per_pass":
+                      "p50_us": round(r.p50_us), "p99_us": round(r.p99_us), "early_calls": early,
+                      "early_env": os.environ.get("SDFS_Q_EARLY", "default"), "mix": os.environ.get("MASK_BITS", "12"),
+                      "calls_per_pass":
                       round((b1[1] - b0[1]) / max(b1[0] - b0[0], 1), 1), **e.queue_timing(), "cgroup": thr}),
           flush=True)
     e.destroy()

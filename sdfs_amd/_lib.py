@@ -113,6 +113,7 @@ SIGNATURES = {
                                                   ctypes.c_uint64, _P(DevOut), _vp]),
     "sdfs_cdc_stream_sync": (ctypes.c_int, [_vp]),
     "sdfs_cdc_queue_stats": (ctypes.c_int, [_vp, _u64p, _u64p]),
+    "sdfs_cdc_queue_early": (ctypes.c_int, [_vp, _u64p]),
     "sdfs_cdc_queue_timing": (ctypes.c_int, [_vp, _P(ctypes.c_double), _P(ctypes.c_double), _P(ctypes.c_double)]),
     "sdfs_cdc_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "sdfs_cdc_set_timing_mask": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32]),

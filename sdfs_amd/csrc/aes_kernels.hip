@@ -793,9 +793,12 @@ int sdfs_cdc_aes_create(int device, const uint8_t* key, uint32_t key_len, sdfs_c
     memcpy(img.data(), t.te0, 1024);
     memcpy(img.data() + 256, t.td0, 1024);
     memcpy(img.data() + 512, t.isb, 1024);
+    // the upload runs on the component's own non-blocking stream, never the legacy null stream
+    // (which would wait for the CDC queue's blocking lane streams)
     if (z->tabs.ensure(768) != hipSuccess ||
-        hipMemcpy(z->tabs.p, img.data(), 768 * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess || z->order.init() != hipSuccess) {
+        hipStreamCreateWithFlags(&z->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMemcpyAsync(z->tabs.p, img.data(), 768 * 4, hipMemcpyHostToDevice, z->stream) != hipSuccess ||
+        hipStreamSynchronize(z->stream) != hipSuccess || z->order.init() != hipSuccess) {
         z->tabs.release();
         if (z->stream) (void)hipStreamDestroy(z->stream);
         delete z;

@@ -1402,6 +1402,17 @@ __device__ __forceinline__ void store_digest(const HashArgs& a, uint32_t slot, u
     const uint4 d1 = make_uint4(dig[4], dig[5], dig[6], dig[7]);
     out[0] = d0;
     out[1] = d1;
+    if (a.done_ctr) {
+        // a queue pass: the digest went to the pinned image; the buffer's last chunk publishes
+        // the buffer (its header was copied to the image before this kernel started).  The
+        // release fence (system scope, no acquire half: nothing here reads what others wrote)
+        // makes this lane's digest visible to the host before its count; the finisher's count
+        // saw every other lane's fenced digest, so its ready word follows all of them.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        const uint32_t c = a.counts[b];
+        if (atomicAdd(a.done_ctr + b, 1u) + 1u == c)
+            __hip_atomic_store(a.ready + b, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (a.records) {
         const uint64_t r = (uint64_t)a.rec_base[b] + k;
         if (r < a.records_cap) {
@@ -1571,6 +1582,25 @@ void chunk_hash_kernel(HashArgs a) {
     if constexpr ((ABL & 32) != 0) {  // LDS only in the DMA-prefetch form
         __shared__ __attribute__((aligned(16))) uint8_t pf_lds[BS / 64 * 4096];
         wave_lds = (lds_u8*)pf_lds + 4096 * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    }
+    if constexpr ((ABL & 128) != 0) {
+        // measurement (sweep variant 50): the wave's wall-clock and shader-clock span and where it
+        // ran (HW_ID: wave/SIMD/CU/SE; XCC_ID), written by its first lane
+        const uint64_t r0 = wall_clock64(), c0 = clock64();
+        hash_task<ALGO, ABL & ~128, PF>(a, i, wave_lds);
+        const uint64_t c1 = clock64(), r1 = wall_clock64();
+        if ((threadIdx.x & 63) == 0 && a.stamps) {
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);    // HW_REG_HW_ID
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID
+            uint64_t* st = a.stamps + 8ull * (i >> 6);
+            st[0] = r0;
+            st[1] = c0;
+            st[2] = r1;
+            st[3] = c1;
+            st[4] = (uint64_t)xcc << 32 | hw;
+            st[5] = sha_blocks(a.clens[a.tasks[i]]);
+        }
+        return;
     }
     hash_task<ALGO, ABL, PF>(a, i, wave_lds);
 }

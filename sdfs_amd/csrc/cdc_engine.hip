@@ -231,6 +231,8 @@ struct QSlotDev {
     // layout of the batch in flight (read by the callers)
     uint32_t n = 0, nh = 0, dcap = 0;
     uint64_t digests_at = 0, hdig_at = 0, img_bytes = 0;
+    uint64_t ready_at = 0;  // pinned ready words (early completion), one per request, past the largest image
+    bool early = false;     // the batch in flight completes its getChunks requests early
     std::string err;  // message of a failed launch/wait (set on the queue's threads)
 };
 
@@ -252,6 +254,7 @@ struct DevEngine {
     bool small_seg = true;                   // short scan segments for small batches (tuning: SDFS_SMALL_SEG)
     uint32_t small_seg_len = kSmallBatchSeg;  // their length (tuning: SDFS_SMALL_SEG_LEN, a multiple of 256)
     uint32_t tiny_seg_len = kTinyBatchSeg;    // below 32 MiB (tuning: SDFS_TINY_SEG_LEN, a multiple of 64)
+    bool q_early = true;  // queue passes complete each getChunks request when its buffer is done (tuning: SDFS_Q_EARLY=0 = off)
     bool tiny_scan = true;  // passes < 32 MiB: 64/128-byte segments with ScanTiny (tuning: SDFS_TINY_SCAN=0 = off)
     bool long_split = true;                  // latency form for chunks > 32 KiB (tuning: SDFS_LONG_SPLIT)
     bool par_stitch = true;                  // parallel join/place of long buffers' sections (tuning: SDFS_PAR_STITCH)
@@ -410,6 +413,24 @@ void t_end(DevEngine* e, int i, hipStream_t st) {
     if (e->run && i >= 0) (void)hipEventRecord(e->run->ev[2 * i + 1], st);
 }
 
+#ifdef SDFS_TUNING
+// measurement only: per-wave stamps of fingerprint variant 50 go here (sdfs_cdc_tuning_set_stamps)
+uint64_t* g_stamps = nullptr;
+#endif
+
+// Early completion of a coalescing-queue pass (HashArgs::done_ctr): the pinned image's header
+// (counts | starts | lens | flags) is copied before the fingerprint runs, the digests go straight
+// into the pinned image, and each buffer's ready word is set as its last chunk is stored.
+struct EarlyDone {
+    const void* hdr_src = nullptr;  // device result image
+    void* hdr_dst = nullptr;        // pinned result image
+    uint64_t hdr_bytes = 0;         // [0, hdr_bytes): its header (a multiple of 16)
+    uint32_t* ready = nullptr;      // pinned ready words, one per buffer
+    uint32_t seq = 0;               // the pass's number (what a ready word is set to)
+};
+
+inline uint32_t early_words(const EarlyDone* early, uint32_t nbuf) { return early ? (nbuf + 3u) & ~3u : 0u; }
+
 // Workspace needs of one pipeline run.
 WsNeed pipeline_need(const DevEngine* e, uint64_t data_bytes, uint32_t nbuf, uint32_t uniform_len, uint32_t cap,
                      uint64_t max_buf_len, uint32_t* sec_len_out, uint32_t* nsec_out, uint32_t* spec_cap_out) {
@@ -439,7 +460,7 @@ WsNeed pipeline_need(const DevEngine* e, uint64_t data_bytes, uint32_t nbuf, uin
 int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
                  const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
                  const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, uint32_t sec_len, uint32_t nsec,
-                 uint32_t spec_cap, uint32_t* ovf_to = nullptr) {
+                 uint32_t spec_cap, uint32_t* ovf_to = nullptr, const EarlyDone* early = nullptr) {
     e->run = nullptr;
     if (e->timing_slots > 0) {
         e->run = &e->ev_runs[e->runs_recorded % e->timing_slots];
@@ -475,12 +496,18 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     // lane, down to 64 bytes, scanned by ScanTiny (64-byte blocks): a lone buffer 21.5 -> 10.4 us
     // (profiles/r05/tiny_scan/).  Passes of 16-32 MiB keep 256 (more lanes than one wave per SIMD:
     // the warm-up would only add work).
+    // Segments shorter than the scan form's block only go to ScanTiny (its 64-byte blocks);
+    // any other form scans whole blocks, so its segments stay multiples of its block.
+    const bool tiny_ok = e->tiny_scan && e->scan_variant == 0;
+    const uint32_t blk = e->scan_info.blk;
     uint32_t small_len = e->small_seg_len;
     if (full_segs < (uint64_t)e->num_cus * 4 * 8) {
         uint32_t t = e->tiny_seg_len;
-        if (e->tiny_scan) {
+        if (tiny_ok) {
             const uint64_t per_lane = data_bytes / ((uint64_t)e->num_cus * 4 * 64);
             while (t > 64 && t % 128 == 0 && t / 2 >= per_lane) t /= 2;
+        } else {
+            t = (t + blk - 1) / blk * blk;
         }
         if (small_len > t && small_len % t == 0) small_len = t;
     }
@@ -495,7 +522,10 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     if (front && e->front_recorded) HIP_TRY(hipStreamWaitEvent(s, e->ev_front, 0));
     {
         const int t = t_begin(e, K_PREP, s);
-        HIP_TRY(launch_prep_zero(w->small.p, kSmall + 8, ovf_to, s));
+        // (+ the per-buffer chunk counters of early completion, behind the fixed words)
+        const uint32_t zw = kSmall + 8 + early_words(early, nbuf);
+        if (!w->small.fits(zw)) return fail(SDFS_CDC_EHIP, "internal: workspace has no early-completion counters");
+        HIP_TRY(launch_prep_zero(w->small.p, zw, ovf_to, s));
         if (!uniform_len) HIP_TRY(launch_seg_prefix(d_lens, nbuf, seg_len, w->seg_prefix.p, s));
         t_end(e, t, s);
     }
@@ -578,13 +608,16 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
         }
     }
     // one wave = one buffer: the scan kernel resolves the cuts in its epilogue
+    // (the fused and piece walks read the scan's per-segment state, so a segment is whole blocks:
+    // a uniform pass of 4 or 8 KiB buffers at 64- or 128-byte segments takes ScanTiny + the walk)
     const bool fused = e->scan_info.fuse && uniform_len && (e->scan_info.chains == 1 || e->scan_info.fuse == 2) &&
-                       (uint64_t)uniform_len == 64ull * seg_len && seg_len < 0xFFFFu;
+                       (uint64_t)uniform_len == 64ull * seg_len && seg_len < 0xFFFFu && seg_len % blk == 0;
     // long uniform buffers whose sections are exactly one wave's 64 segments: the scan's epilogue
     // walks every section speculatively from the lanes' summaries (no spec kernel)
     const bool piece = !fused && e->piece_walk && e->par_stitch && sec_len && uniform_len && w->seg_sum.p &&
                        e->scan_info.fuse == 2 && e->scan_info.chains == 1 &&
-                       sec_len == 64ull * seg_len && uniform_len % sec_len == 0 && seg_len < 0xFFFF;
+                       sec_len == 64ull * seg_len && uniform_len % sec_len == 0 && seg_len < 0xFFFF &&
+                       seg_len % blk == 0;
     if (piece) {
         ra.spec_from_scan = 1;
         ra.seg_sum = w->seg_sum.p;
@@ -609,10 +642,12 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     grid = std::max<uint64_t>(grid, 1);
     {
         const int t = t_begin(e, K_SCAN, s);
-        if (e->tiny_scan && e->scan_variant == 0 && seg_len < 256 && !sa.fuse_resolve)
+        if (seg_len % blk != 0) {
+            if (!tiny_ok || sa.fuse_resolve) return fail(SDFS_CDC_EINVAL, "internal: segment %u not whole blocks", seg_len);
             HIP_TRY(launch_scan_tiny(sa, (int)e->prm.window, pk, (int)grid, (int)block, s));
-        else
+        } else {
             HIP_TRY(launch_scan(sa, (int)e->prm.window, pk, e->scan_variant, (int)grid, (int)block, s));
+        }
         t_end(e, t, s);
     }
     if (!fused) {
@@ -680,6 +715,18 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
     ha.algo = e->prm.hash_algo;
     ha.wave_ctr = w->small.p + 2 * kMaxBins + 2;  // zeroed with the rest of `small` above
     ha.persist_grid = (uint32_t)(e->num_cus * e->hash_wg_per_cu);
+#ifdef SDFS_TUNING
+    ha.stamps = g_stamps;
+#endif
+    if (early) {
+        // the header the callers read is final once the walk and scatter ran: into the pinned
+        // image now, in stream order before the fingerprint (whose digests go there directly)
+        HIP_TRY(launch_copy_out(early->hdr_src, early->hdr_dst, early->hdr_bytes, s));
+        ha.done_ctr = w->small.p + kSmall + 8;  // zeroed by the prep above
+        ha.counts = out->counts;
+        ha.ready = early->ready;
+        ha.seq = early->seq;
+    }
     {
         // chunks of more than kLongBlocks SHA blocks (a maxLen above 32 KiB: the backup profile)
         // head the longest-first list; after the scatter, cursor[b] = tasks in bins >= b, so
@@ -721,7 +768,7 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
 int device_run(DevEngine* e, const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_offs,
                const uint32_t* d_lens, uint32_t nbuf, uint32_t uniform_len, uint64_t buffer_id_base,
                const sdfs_cdc_dev_out* out, hipStream_t s, uint64_t max_buf_len, const uint32_t** ovf_dev,
-               Workspace* own = nullptr, uint32_t* ovf_to = nullptr) {
+               Workspace* own = nullptr, uint32_t* ovf_to = nullptr, const EarlyDone* early = nullptr) {
     if (!out || !out->counts || !out->starts || !out->lens || !out->digests || !out->total)
         return fail(SDFS_CDC_EINVAL, "incomplete sdfs_cdc_dev_out");
     if (uniform_len && (uniform_len & 63)) return fail(SDFS_CDC_EINVAL, "uniform_len must be a multiple of 64");
@@ -736,7 +783,7 @@ int device_run(DevEngine* e, const uint8_t* d_data, uint64_t data_bytes, const u
     int rc = ws_acquire(e, nd, s, &w, own);
     if (rc) return rc;
     rc = run_pipeline(e, w, d_data, data_bytes, d_offs, d_lens, nbuf, uniform_len, buffer_id_base, out, s, max_buf_len,
-                      sec_len, nsec, spec_cap, ovf_to);
+                      sec_len, nsec, spec_cap, ovf_to, early);
     const int rr = ws_release(w, s);  // even after a failed enqueue: what was enqueued completes first
     if (ovf_dev) *ovf_dev = w->overflow();
     return rc ? rc : rr;
@@ -1012,7 +1059,8 @@ struct QueueBackend {
         s.dev = d;
         int rc = pinned_ensure(&s.in, &s.cap, slot_bytes);
         if (!rc) rc = pinned_ensure(&d->pin_meta, &d->pin_meta_n, (size_t)max_reqs * 24 + 64);
-        if (!rc) rc = pinned_ensure(&d->pin_out, &d->pin_out_n, image_bytes(max_reqs, out_entries, max_reqs));
+        d->ready_at = image_bytes(max_reqs, out_entries, max_reqs);
+        if (!rc) rc = pinned_ensure(&d->pin_out, &d->pin_out_n, d->ready_at + 4ull * max_reqs);
         if (rc) return rc;
         s.cap = slot_bytes;
         HIP_TRY(d->data.ensure(slot_bytes));
@@ -1022,7 +1070,7 @@ struct QueueBackend {
         HIP_TRY(d->dimg.ensure(image_bytes(max_reqs, out_entries, max_reqs)));
         Workspace& w = d->ws;
         HIP_TRY(w.bitmap.ensure(slot_bytes / 32 + 2));
-        HIP_TRY(w.small.ensure(kSmall + 8));
+        HIP_TRY(w.small.ensure(kSmall + 8 + ((max_reqs + 3) & ~3u)));  // + early-completion counters
         HIP_TRY(w.rec_base.ensure(max_reqs));
         HIP_TRY(w.tasks.ensure(out_entries));
         HIP_TRY(w.seg_prefix.ensure(max_reqs + 1ull));
@@ -1150,8 +1198,21 @@ struct QueueBackend {
             // every CHUNK_LENGTH flush buffer (the common case) takes the uniform layout and the
             // fused cut walk; mixed lengths (write-accelerator runs) the ragged one
             const uint32_t ul = uniform_pass ? s.uniform_len : 0;
+            // Early completion: the header goes to the pinned image before the fingerprint, the
+            // digests straight into it, and each buffer's ready word is set when its last chunk
+            // is stored (HashArgs::done_ctr); the completer's poll wakes that caller then.
+            EarlyDone ed;
+            d->early = e->q_early;
+            if (d->early) {
+                out.digests = d->pin_out + d->digests_at;
+                ed.hdr_src = d->dimg.p;
+                ed.hdr_dst = d->pin_out;
+                ed.hdr_bytes = d->digests_at;
+                ed.ready = reinterpret_cast<uint32_t*>(d->pin_out + d->ready_at);
+                ed.seq = (uint32_t)s.seq;
+            }
             rc = device_run(e, d->data.p, s.lo, ul ? nullptr : d->meta64.p, ul ? nullptr : d->meta32.p, n, ul, 0,
-                            &out, st, s.max_chunk_len, nullptr, &d->ws, dflag);
+                            &out, st, s.max_chunk_len, nullptr, &d->ws, dflag, d->early ? &ed : nullptr);
             if (rc) return rc;
         }
         if (nh) {
@@ -1159,7 +1220,10 @@ struct QueueBackend {
                               d->dimg.p + d->hdig_at, st, &d->ws);
             if (rc) return rc;
         }
-        HIP_TRY(launch_copy_out(d->dimg.p, d->pin_out, d->img_bytes, st));
+        if (n && d->early)  // header and digests are in the pinned image already: only getHash's
+            HIP_TRY(launch_copy_out(d->dimg.p + d->hdig_at, d->pin_out + d->hdig_at, d->img_bytes - d->hdig_at, st));
+        else
+            HIP_TRY(launch_copy_out(d->dimg.p, d->pin_out, d->img_bytes, st));
         HIP_TRY(hipEventRecord(d->kdone, st));
         return SDFS_CDC_OK;
     }
@@ -1170,6 +1234,31 @@ struct QueueBackend {
         const int rc = wait_impl(d);
         if (rc && d->err.empty()) d->err = g_last_error;
         return rc;
+    }
+
+    // Runs on the queue's completer thread (host_queue.h Backend::poll): a chunk request is final
+    // once its ready word holds this pass's number (the kernel set it after a system-scope fence
+    // behind the buffer's last digest; its header was in the image before the fingerprint ran),
+    // unless the walk flagged a slot overflow, which the batch's end reports.
+    int poll(QSlot& s, uint8_t* ready, bool* finished) {
+        auto* d = static_cast<QSlotDev*>(s.dev);
+        if (d->early && d->n) {
+            const volatile uint32_t* rd = reinterpret_cast<const volatile uint32_t*>(d->pin_out + d->ready_at);
+            const volatile uint32_t* pflag = reinterpret_cast<const volatile uint32_t*>(d->pin_out) + d->n + 2ull * d->n * d->dcap;
+            const uint32_t seq = (uint32_t)s.seq;
+            for (uint32_t i = 0; i < d->n; i++)
+                if (!ready[i] && rd[i] == seq) {
+                    std::atomic_thread_fence(std::memory_order_acquire);
+                    if (*pflag == 0) ready[i] = 1;
+                }
+        }
+        const hipError_t q = hipEventQuery(d->kdone);
+        if (q == hipErrorNotReady && d->early && d->n) {
+            *finished = false;
+            return SDFS_CDC_OK;
+        }
+        *finished = true;  // done, failed, or nothing to complete early: finish as wait does
+        return wait(s);
     }
 
     // Kernels (the last one wrote the pinned result image) done -> done.
@@ -1304,6 +1393,7 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_HASH_SPLIT")) e->hash_split = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SMALL_SEG")) e->small_seg = atoi(v) != 0;
     if (const char* v = getenv("SDFS_TINY_SCAN")) e->tiny_scan = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_Q_EARLY")) e->q_early = atoi(v) != 0;
     if (const char* v = getenv("SDFS_TINY_SEG_LEN")) {
         const int n = atoi(v);
         if (n >= 64 && n % 64 == 0) e->tiny_seg_len = (uint32_t)n;
@@ -1344,9 +1434,12 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
         return fail(SDFS_CDC_EINVAL, "the divisor predicate runs on the production scan only");
     std::vector<uint8_t> img = build_table_image(p->poly, p->window, e->scan_info.copies, e->scan_info.mirror != 0,
                                                  e->scan_info.pop_swap != 0);
-    if (e->zero_page.ensure(256) != hipSuccess || hipMemset(e->zero_page.p, 0, 256) != hipSuccess ||
+    // on the engine's own non-blocking stream: the queue lanes are blocking streams (CU-masked),
+    // so anything on the legacy null stream would wait for their passes in flight
+    if (e->zero_page.ensure(256) != hipSuccess || hipMemsetAsync(e->zero_page.p, 0, 256, e->stream) != hipSuccess ||
         e->tab_image.ensure(img.size()) != hipSuccess ||
-        hipMemcpy(e->tab_image.p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpyAsync(e->tab_image.p, img.data(), img.size(), hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
         return fail(SDFS_CDC_ENOMEM, "table upload failed");
     *out = std::move(e);
     return SDFS_CDC_OK;
@@ -1998,6 +2091,17 @@ int sdfs_cdc_queue_stats(sdfs_cdc_engine* e, uint64_t* batches, uint64_t* reques
     return SDFS_CDC_OK;
 }
 
+int sdfs_cdc_queue_early(sdfs_cdc_engine* e, uint64_t* early) {
+    USE_OR_FAIL(u, e);
+    uint64_t n = 0;
+    for (auto& d : u.set().devs) {
+        std::lock_guard<std::mutex> lk(d->q_init);
+        if (d->q) n += d->q->early();
+    }
+    if (early) *early = n;
+    return SDFS_CDC_OK;
+}
+
 int sdfs_cdc_queue_timing(sdfs_cdc_engine* e, double* fill_us, double* copy_us, double* device_us) {
     USE_OR_FAIL(u, e);
     double f = 0, c = 0, dv = 0, wsum = 0;
@@ -2121,5 +2225,14 @@ int sdfs_cdc_allgather_records(sdfs_cdc_engine* e, uint8_t* const* records, cons
         return api->all_gather(records[i], gathered[i], m * SDFS_CDC_RECORD_BYTES, kNcclUint8, c->comms[i], st(i));
     });
 }
+
+#ifdef SDFS_TUNING
+// measurement only (tuning library): where fingerprint variant 50 writes its per-wave stamps
+// (8 u64 per 64 tasks; device memory the caller owns, or null)
+int sdfs_cdc_tuning_set_stamps(void* dev_ptr) {
+    g_stamps = static_cast<uint64_t*>(dev_ptr);
+    return SDFS_CDC_OK;
+}
+#endif
 
 }  // extern "C"

@@ -168,6 +168,18 @@ struct HashArgs {
     // 0 = one lane per chunk throughout
     const uint32_t* nlong;
     uint32_t max_long;
+    // Early completion of a coalescing-queue pass (host_queue.h): `digests` points into the pass's
+    // pinned result image; a buffer whose last chunk's digest is stored gets its ready word set to
+    // `seq` (after a system-scope fence), so its caller returns before the pass's longest chunk
+    // is done.  done_ctr: [nbuf] zeroed per-buffer counters of stored chunks; counts: [nbuf] the
+    // buffers' chunk counts (device).  done_ctr == null: off.
+    uint32_t* done_ctr;
+    const uint32_t* counts;
+    uint32_t* ready;
+    uint32_t seq;
+    // measurement only (tuning build, fingerprint variant 50): per wave {wall clock, shader clock}
+    // at its start and end, and its HW_ID / XCC_ID, 8 u64 per wave (scripts/hash_stamps.py)
+    uint64_t* stamps;
 };
 
 // Longest-first order of arbitrary chunk extents (getHash in bulk): tasks[] = extent indices,
@@ -211,6 +223,9 @@ hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipSt
 hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t stream, bool packed = true);
 hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t stream);
 hipError_t launch_copy_out(const void* src, void* dst, uint64_t bytes, hipStream_t stream);
+// Early completion (HashArgs::done_ctr): everything the pinned image's header needs before the
+// fingerprint runs -- a kernel that copies [0, bytes) of the device image to pinned memory.
+// (launch_copy_out itself, launched before the fingerprint.)
 hipError_t launch_prep_zero(uint32_t* small, uint32_t words, uint32_t* flag, hipStream_t stream);
 constexpr uint64_t kSmallScatterSlots = 65536;  // chunk slots up to which prefix + scatter run fused
 hipError_t launch_prefix_scatter_small(const PrefixArgs& a, const ScatterArgs& c, hipStream_t stream);

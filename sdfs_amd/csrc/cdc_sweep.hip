@@ -307,6 +307,9 @@ hipError_t launch_hash_sweep(const HashArgs& a, uint64_t max_tasks, int variant,
               // wrong digests): the clock of the same VALU work without the HBM traffic
         hipLaunchKernelGGL((chunk_hash_kernel<0, 16 | 1, 256, true, true>), dim3(blocks), dim3(256), 0, s, a);
         break;
+    case 50:  // production kernel + per-wave clock stamps (HashArgs::stamps; scripts/hash_stamps.py)
+        hipLaunchKernelGGL((chunk_hash_kernel<0, 16 | 128, 256, true, true>), dim3(blocks), dim3(256), 0, s, a);
+        break;
     case 31:  // production kernel without the issue priority for waves of long chunks
         hipLaunchKernelGGL((chunk_hash_kernel<0, 16, 256, true, false>), dim3(blocks), dim3(256), 0, s, a);
         break;

@@ -305,7 +305,8 @@ struct sdfs_cdc_index {
     IxBuf<IndexSlot> table;
     IxBuf<uint64_t> used;  // [1] device count of fingerprints held
     IxBuf<uint32_t> ltab, lcount, lslot, gidx, isnew, bsum, overflow;
-    hipStream_t last = nullptr;
+    hipStream_t own = nullptr;   // the index's own non-blocking stream: set-up and readbacks
+    hipStream_t last = nullptr;  // the stream of the latest batch (own until one comes)
     StreamOrder order;  // batches apply in call order whatever streams they come on
     std::mutex mu;
 };
@@ -330,10 +331,12 @@ int sdfs_cdc_index_create(int device, uint64_t capacity, sdfs_cdc_index** out) {
     IX_TRY(hipSetDevice(device));
     auto* ix = new sdfs_cdc_index();
     ix->device = device;
-    if (ix->order.init() != hipSuccess) {
+    if (ix->order.init() != hipSuccess || hipStreamCreateWithFlags(&ix->own, hipStreamNonBlocking) != hipSuccess) {
+        ix->order.destroy();
         delete ix;
-        return fail_status(SDFS_CDC_EHIP, "event creation failed");
+        return fail_status(SDFS_CDC_EHIP, "event or stream creation failed");
     }
+    ix->last = ix->own;
     ix->slots = next_pow2(capacity + capacity / 7 + 1);
     ix->max_fill = ix->slots - ix->slots / 8;
     if (ix->table.ensure(ix->slots) != hipSuccess || ix->used.ensure(1) != hipSuccess ||
@@ -342,9 +345,12 @@ int sdfs_cdc_index_create(int device, uint64_t capacity, sdfs_cdc_index** out) {
         return fail_status(SDFS_CDC_ENOMEM, "index allocation (%llu slots) failed",
                            (unsigned long long)ix->slots);
     }
-    if (hipMemset(ix->table.p, 0, ix->slots * sizeof(IndexSlot)) != hipSuccess ||
-        hipMemset(ix->used.p, 0, sizeof(uint64_t)) != hipSuccess ||
-        hipMemset(ix->overflow.p, 0, sizeof(uint32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    // Nothing here or below runs on the legacy null stream or synchronises the device: the CDC
+    // queue's lanes are blocking streams, and a null-stream operation would wait for their passes.
+    if (hipMemsetAsync(ix->table.p, 0, ix->slots * sizeof(IndexSlot), ix->own) != hipSuccess ||
+        hipMemsetAsync(ix->used.p, 0, sizeof(uint64_t), ix->own) != hipSuccess ||
+        hipMemsetAsync(ix->overflow.p, 0, sizeof(uint32_t), ix->own) != hipSuccess ||
+        hipStreamSynchronize(ix->own) != hipSuccess) {
         sdfs_cdc_index_destroy(ix);
         return fail_status(SDFS_CDC_EHIP, "index initialisation failed");
     }
@@ -355,12 +361,16 @@ int sdfs_cdc_index_create(int device, uint64_t capacity, sdfs_cdc_index** out) {
 int sdfs_cdc_index_destroy(sdfs_cdc_index* ix) {
     if (!ix) return SDFS_CDC_OK;
     (void)hipSetDevice(ix->device);
-    (void)hipDeviceSynchronize();
+    // batches are chained in call order (StreamOrder), so the latest one's stream finishing means
+    // every earlier one has
+    if (ix->last) (void)hipStreamSynchronize(ix->last);
+    if (ix->own) (void)hipStreamSynchronize(ix->own);
     ix->table.release();
     ix->used.release();
     for (auto* b : {&ix->ltab, &ix->lcount, &ix->lslot, &ix->gidx, &ix->isnew, &ix->bsum, &ix->overflow})
         b->release();
     ix->order.destroy();
+    if (ix->own) (void)hipStreamDestroy(ix->own);
     delete ix;
     return SDFS_CDC_OK;
 }
@@ -380,8 +390,9 @@ int sdfs_cdc_index_put_records(sdfs_cdc_index* ix, const uint8_t* d_records, uin
         IX_TRY(hipStreamSynchronize(s));
         uint64_t used = 0;
         uint32_t ovf = 0;
-        IX_TRY(hipMemcpy(&used, ix->used.p, sizeof(used), hipMemcpyDeviceToHost));
-        IX_TRY(hipMemcpy(&ovf, ix->overflow.p, sizeof(ovf), hipMemcpyDeviceToHost));
+        IX_TRY(hipMemcpyAsync(&used, ix->used.p, sizeof(used), hipMemcpyDeviceToHost, ix->own));
+        IX_TRY(hipMemcpyAsync(&ovf, ix->overflow.p, sizeof(ovf), hipMemcpyDeviceToHost, ix->own));
+        IX_TRY(hipStreamSynchronize(ix->own));
         if (ovf) return fail_status(SDFS_CDC_ECAP, "index overflowed");
         ix->used_ub = used;
         if (used + n_max > ix->max_fill)
@@ -473,7 +484,8 @@ int sdfs_cdc_index_size(sdfs_cdc_index* ix, uint64_t* used, uint64_t* capacity) 
     IX_TRY(hipSetDevice(ix->device));
     IX_TRY(hipStreamSynchronize(ix->last));
     uint64_t u = 0;
-    IX_TRY(hipMemcpy(&u, ix->used.p, sizeof(u), hipMemcpyDeviceToHost));
+    IX_TRY(hipMemcpyAsync(&u, ix->used.p, sizeof(u), hipMemcpyDeviceToHost, ix->own));
+    IX_TRY(hipStreamSynchronize(ix->own));
     ix->used_ub = u;
     if (used) *used = u;
     if (capacity) *capacity = ix->max_fill;

@@ -33,7 +33,12 @@
 #include <deque>
 #include <mutex>
 #include <thread>
+#include <type_traits>
+#include <utility>
 #include <vector>
+#ifdef __linux__
+#include <sys/prctl.h>
+#endif
 
 namespace sdfs {
 
@@ -170,13 +175,26 @@ constexpr int kQueueTooBig = -1001;   // the request exceeds the per-request lim
 //                          `lane` (one stream per lane; dispatcher thread)
 //   int  wait(QSlot&)      block until that work completed (the lane's completer thread)
 //   void release(QSlot&)   free what prepare allocated
-// launch and wait run without the queue lock.
+//   int  poll(QSlot&, uint8_t* ready, bool* finished)   OPTIONAL, non-blocking progress of a
+//                          launched slot: sets ready[i] = 1 for each getChunks request i (the
+//                          slot's chunks[i]) whose results are final before the whole batch is
+//                          (its buffer's last chunk was fingerprinted); *finished = true once the
+//                          batch completed, and then the return value is its status as wait's.
+//                          A backend with poll lets each caller go as soon as its own buffer is
+//                          done instead of when the batch's longest chunk is.
+// launch, wait and poll run without the queue lock.
 //
 // Dispatch policy.  A batch costs the device about the same time whatever its size (its
 // longest chunk's serial SHA-256 chain sets it), so batches should be as large as the callers
 // allow, but no caller should wait long: the dispatcher launches the OPEN slot onto an idle lane
 // when nothing is in flight, or when it holds its share of the callers (active callers /
 // lanes), or when it is full, or when its first request has waited `linger_us`.
+template <class B, class = void>
+struct has_poll : std::false_type {};
+template <class B>
+struct has_poll<B, std::void_t<decltype(std::declval<B&>().poll(std::declval<QSlot&>(), (uint8_t*)nullptr, (bool*)nullptr))>>
+    : std::true_type {};
+
 template <class Backend>
 class CoalescingQueue {
   public:
@@ -186,11 +204,12 @@ class CoalescingQueue {
         uint32_t max_reqs = 1024;  // requests per slot (the backend sizes its result image for this)
         uint64_t max_req_bytes = 0;  // larger requests bypass the queue (0 = cap / 2)
         uint32_t linger_us = 250;  // longest a request waits for company while a batch is in flight
+        uint32_t poll_us = 10;     // early completion (Backend::poll): the completer's poll period
     };
 
     CoalescingQueue(Backend& b, Config c)
         : b_(b), c_(c), slots_(c.nslots), done_cv_(c.nslots), flight_(c.lanes), comp_cv_(c.lanes),
-          lane_busy_(c.lanes, 0) {}
+          lane_busy_(c.lanes, 0), early_(c.lanes) {}
     ~CoalescingQueue() { shutdown(); }
     CoalescingQueue(const CoalescingQueue&) = delete;
     CoalescingQueue& operator=(const CoalescingQueue&) = delete;
@@ -304,7 +323,9 @@ class CoalescingQueue {
         lk.unlock();
         const int ret = frc ? frc : read(*s, r, r.status);
         lk.lock();
-        if (--s->readers == 0) {
+        // an early-completed caller may leave while its batch is still on the device: the slot
+        // is free once its last reader has left AND the batch has completed
+        if (--s->readers == 0 && s->state == QSlot::kDone) {
             s->state = QSlot::kFree;
             admit_waiting();
         }
@@ -320,6 +341,11 @@ class CoalescingQueue {
     uint64_t requests() {
         std::lock_guard<std::mutex> lk(m_);
         return served_;
+    }
+    // getChunks requests completed before their batch (Backend::poll)
+    uint64_t early() {
+        std::lock_guard<std::mutex> lk(m_);
+        return early_done_;
     }
     // mean microseconds per completed batch: open -> closed (filling), closed -> launched (the
     // callers' copies), launched -> completion observed (transfers + kernels)
@@ -472,8 +498,42 @@ class CoalescingQueue {
         for (auto& cv : comp_cv_) cv.notify_all();
     }
 
+    // Waits for a launched slot's batch like Backend::wait, completing each getChunks request as
+    // soon as the backend reports it final (called and returns without the queue lock).
+    int wait_early(QSlot& s, int lane, std::unique_lock<std::mutex>& lk) {
+        std::vector<uint8_t>& rdy = early_[lane];
+        rdy.assign(s.chunks.size(), 0);  // the slot is closed: its request list does not change
+        const int idx = (int)(&s - slots_.data());
+        size_t left = s.chunks.size();
+        for (;;) {
+            bool fin = false;
+            const int rc = b_.poll(s, rdy.data(), &fin);
+            if (fin) return rc;
+            bool any = false;
+            for (size_t i = 0; i < rdy.size(); i++)
+                if (rdy[i] == 1) {
+                    if (!any) lk.lock();
+                    any = true;
+                    rdy[i] = 2;  // completed early: the request may be gone once its caller wakes
+                    s.chunks[i]->status = 0;
+                    s.chunks[i]->done = true;
+                    early_done_++;
+                    left--;
+                }
+            if (any) {
+                done_cv_[idx].notify_all();
+                lk.unlock();
+            }
+            if (left == 0) return b_.wait(s);  // nothing else can complete early
+            std::this_thread::sleep_for(std::chrono::microseconds(c_.poll_us));
+        }
+    }
+
     // One per lane: a lane's batches complete in launch order (one stream).
     void completer(int lane) {
+#ifdef __linux__
+        prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us: the poll period's sleeps stay short
+#endif
         std::unique_lock<std::mutex> lk(m_);
         for (;;) {
             comp_cv_[lane].wait(lk, [&] { return !flight_[lane].empty() || (disp_done_ && inflight_ == 0); });
@@ -482,7 +542,14 @@ class CoalescingQueue {
             flight_[lane].pop_front();
             const int launched_rc = s->status;
             lk.unlock();
-            const int rc = b_.wait(*s);  // always: drains whatever a failed launch enqueued
+            bool polled = false;
+            int rc;
+            if constexpr (has_poll<Backend>::value) {
+                polled = launched_rc == 0;
+                rc = polled ? wait_early(*s, lane, lk) : b_.wait(*s);
+            } else {
+                rc = b_.wait(*s);  // always: drains whatever a failed launch enqueued
+            }
             lk.lock();
             s->status = launched_rc ? launched_rc : rc;
             s->state = QSlot::kDone;
@@ -493,15 +560,20 @@ class CoalescingQueue {
             timed_++;
             inflight_--;
             lane_busy_[lane]--;
-            for (QReq* q : s->chunks) {
-                q->status = s->status;
-                q->done = true;
+            for (size_t i = 0; i < s->chunks.size(); i++) {
+                if (polled && early_[lane][i] == 2) continue;  // completed (and maybe gone) already
+                s->chunks[i]->status = s->status;
+                s->chunks[i]->done = true;
             }
             for (QReq* q : s->hashes) {
                 q->status = s->status;
                 q->done = true;
             }
             done_cv_[s - slots_.data()].notify_all();
+            if (s->readers == 0) {  // every caller completed early and has left
+                s->state = QSlot::kFree;
+                admit_waiting();
+            }
             cv_disp_.notify_all();
             if (disp_done_ && inflight_ == 0)
                 for (auto& cv : comp_cv_) cv.notify_all();
@@ -522,6 +594,7 @@ class CoalescingQueue {
     std::vector<std::deque<QSlot*>> flight_;        // per lane, in launch order
     std::vector<std::condition_variable> comp_cv_;  // per lane
     std::vector<int> lane_busy_;
+    std::vector<std::vector<uint8_t>> early_;  // per lane: its slot's requests completed early (2)
     std::thread disp_;
     std::vector<std::thread> comp_;
     int open_ = -1;
@@ -533,7 +606,7 @@ class CoalescingQueue {
     bool disp_done_ = false;  // the dispatcher has ended (stopping)
     uint64_t max_req_ = 0;
     uint64_t seq_ = 0;
-    uint64_t launched_ = 0, served_ = 0, timed_ = 0;
+    uint64_t launched_ = 0, served_ = 0, timed_ = 0, early_done_ = 0;
     double t_fill_ = 0, t_copy_ = 0, t_dev_ = 0;
 };
 

@@ -1598,7 +1598,10 @@ int sdfs_cdc_lz4_decompress(sdfs_cdc_lz4* z, const uint8_t* src, uint32_t n, uin
     LZ_TRY(hipStreamSynchronize(s));
     if (got != dst_len) return fail_status(SDFS_CDC_EINVAL, "malformed LZ4 block (decoded %d of %u bytes)",
                                            got == kLz4Corrupt ? -1 : (int)got, dst_len);
-    if (dst_len) LZ_TRY(hipMemcpy(dst, z->h_out.p, dst_len, hipMemcpyDeviceToHost));
+    if (dst_len) {  // on the compressor's own non-blocking stream, not the legacy null stream
+        LZ_TRY(hipMemcpyAsync(dst, z->h_out.p, dst_len, hipMemcpyDeviceToHost, s));
+        LZ_TRY(hipStreamSynchronize(s));
+    }
     return SDFS_CDC_OK;
 }
 

@@ -343,6 +343,12 @@ class HipVariableSha256HashEngine:
         check(self._lib.sdfs_cdc_queue_timing(self._h, ctypes.byref(f), ctypes.byref(c), ctypes.byref(d)))
         return {"fill_us": round(f.value, 1), "copy_us": round(c.value, 1), "device_us": round(d.value, 1)}
 
+    def queue_early(self) -> int:
+        """getChunks calls answered before the rest of their GPU pass finished (cumulative)."""
+        n = ctypes.c_uint64()
+        check(self._lib.sdfs_cdc_queue_early(self._h, ctypes.byref(n)))
+        return n.value
+
     def queue_stats(self) -> tuple[int, int]:
         """(GPU passes launched, getChunks/getHash calls served) by the coalescing queue."""
         b, r = ctypes.c_uint64(), ctypes.c_uint64()

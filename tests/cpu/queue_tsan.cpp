@@ -6,7 +6,9 @@
 //
 // Checks: every caller gets exactly its own result (a per-request function of its bytes), the
 // queue really coalesces (fewer batches than requests), slots are reused, and a backend failure
-// reaches every request of the failing batch.  Test infrastructure only.
+// reaches every request of the failing batch.  The backend completes getChunks requests early
+// (Backend::poll), so callers leave while their batch is still running, and a slot is reused only
+// once its batch is done and its last caller has left.  Test infrastructure only.
 #include <algorithm>
 #include <atomic>
 #include <cassert>
@@ -28,6 +30,7 @@ static uint64_t digest_of(const uint8_t* p, uint64_t n, uint64_t salt) {
 
 struct CpuSlot {
     std::vector<uint64_t> chunk_res, hash_res;
+    size_t next = 0;  // early completion: chunk requests computed so far
     bool fail_next = false;
 };
 
@@ -35,6 +38,7 @@ struct CpuBackend {
     uint64_t slot_bytes;
     std::atomic<int> fail_batches{0};  // number of upcoming batches to fail
     std::atomic<int> launches{0};
+    std::atomic<int> early{0};  // chunk requests completed before their batch
 
     int prepare(QSlot& s) {
         s.in = static_cast<uint8_t*>(malloc(slot_bytes));
@@ -61,20 +65,45 @@ struct CpuBackend {
         while (f > 0 && !fail_batches.compare_exchange_weak(f, f - 1)) {
         }
         if (f > 0) d->fail_next = true;
+        // result arrays sized once per batch: early-completed callers read them while the rest
+        // of the batch is still being computed
+        d->chunk_res.assign(s.chunks.size(), 0);
+        d->hash_res.assign(s.hashes.size(), 0);
+        d->next = 0;
         // a "device" that takes a moment, so batches overlap the callers' copies
         std::this_thread::sleep_for(std::chrono::microseconds(50));
+        return 0;
+    }
+    void chunk_result(QSlot& s, CpuSlot* d, size_t i) {
+        const QReq* q = s.chunks[i];
+        assert(q->off % 64 == 0 && q->off + q->len <= s.lo);
+        d->chunk_res[i] = digest_of(s.in + q->off, q->len, 1);
+    }
+    // early completion (host_queue.h Backend::poll): one more chunk request per call, in a
+    // scrambled order; a batch that is going to fail completes nothing early (as on the GPU,
+    // where a failed launch sets no ready word)
+    int poll(QSlot& s, uint8_t* ready, bool* finished) {
+        auto* d = static_cast<CpuSlot*>(s.dev);
+        const size_t n = s.chunks.size();
+        if (d->fail_next || d->next >= n) {
+            *finished = true;
+            return wait(s);
+        }
+        const size_t i = (d->next * 7 + 3) % n;  // a permutation whenever gcd(7, n) == 1
+        d->next++;
+        if (!ready[i] && std::__gcd<size_t>(7, n) == 1) {
+            chunk_result(s, d, i);
+            ready[i] = 1;
+            early++;
+        }
+        *finished = false;
         return 0;
     }
     int wait(QSlot& s) {
         auto* d = static_cast<CpuSlot*>(s.dev);
         if (d->fail_next) return -3;
-        d->chunk_res.assign(s.chunks.size(), 0);
-        d->hash_res.assign(s.hashes.size(), 0);
-        for (size_t i = 0; i < s.chunks.size(); i++) {
-            const QReq* q = s.chunks[i];
-            assert(q->off % 64 == 0 && q->off + q->len <= s.lo);
-            d->chunk_res[i] = digest_of(s.in + q->off, q->len, 1);
-        }
+        for (size_t i = 0; i < s.chunks.size(); i++)
+            if (d->chunk_res[i] == 0) chunk_result(s, d, i);  // those not completed early
         for (size_t j = 0; j < s.hashes.size(); j++) {
             const QReq* q = s.hashes[j];
             assert(q->off % 16 == 0 && q->off >= s.hi && q->off + q->len <= s.cap);
@@ -127,13 +156,14 @@ static int stress(int nthreads, int per_thread, uint64_t slot_bytes, int fail_ba
     for (auto& x : th) x.join();
     const uint64_t batches = q.batches(), reqs = q.requests();
     q.shutdown();
-    printf("threads=%d reqs=%llu batches=%llu failed=%d bad=%d\n", nthreads, (unsigned long long)reqs,
-           (unsigned long long)batches, failed.load(), bad.load());
+    printf("threads=%d reqs=%llu batches=%llu failed=%d bad=%d early=%d\n", nthreads, (unsigned long long)reqs,
+           (unsigned long long)batches, failed.load(), bad.load(), b.early.load());
     if (bad) return 2;
     if (reqs != (uint64_t)nthreads * per_thread) return 3;
     if (fail_batches == 0 && failed) return 4;
     if (fail_batches > 0 && failed == 0) return 5;
     if (nthreads >= 8 && batches >= reqs) return 6;  // concurrent callers must share batches
+    if (nthreads >= 8 && b.early == 0) return 8;      // early completion must have happened
     return 0;
 }
 

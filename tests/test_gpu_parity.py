@@ -210,6 +210,51 @@ def test_small_batch_walk_list_and_ballot_forms():
             assert_same(e.chunk_arrays(bufs[b].tobytes()), O.chunk(bufs[b].tobytes(), O.Params(**prm)), ("queue", b))
 
 
+@pytest.mark.parametrize("buf_len", [4096, 8192, 16384])
+@pytest.mark.parametrize("mix", [(4095, 0xFFF), (2047, 0x7FF)], ids=["default", "mix4k"])
+def test_uniform_small_buffers_every_segment_route(buf_len, mix):
+    """Uniform batches of 4, 8 and 16 KiB buffers: a wave's 64 segments are one buffer when the
+    segment is buf_len / 64 (64, 128 or 256 bytes), which only the 256-byte segment may take as
+    the scan's fused walk (whole ScanProd blocks); 64/128-byte segments take ScanTiny + the walk.
+    Small (lone-pass) and 16 MiB device batches, a uniform host batch and concurrent single calls
+    of one buffer each, all vs the oracle."""
+    prm = P(min_len=mix[0], pred_mask=mix[1])
+    e = engine_for(prm)
+    for nbuf in (64, (16 << 20) // buf_len):
+        bps = 16
+        batch = DeviceBatch(e, nbuf=nbuf, buf_len=buf_len)
+        batch.fill_streams(first_stream=70, bufs_per_stream=bps)
+        batch.run()
+        counts, st, ln, dg, total = batch.host_results()
+        assert total == counts.sum()
+        sample = None if nbuf <= 64 else sorted(set(np.random.default_rng(buf_len).integers(0, nbuf, 48).tolist()))
+        _check_batch_against_oracle(batch, counts, st, ln, dg, prm, bps, 70, sample)
+    n = 96
+    base = O.synth(SYNTH_SEED, 71, 0, n * buf_len)
+    offs = np.arange(n, dtype=np.uint64) * buf_len
+    lens = np.full(n, buf_len, np.uint32)
+    counts, st, ln, dg = e.chunk_batch(base, offs, lens)
+    exp = [O.chunk(base[b * buf_len:(b + 1) * buf_len].tobytes(), O.Params(**prm)) for b in range(n)]
+    for b in range(n):
+        assert_same((st[b, :counts[b]], ln[b, :counts[b]], dg[b, :counts[b]]), exp[b], b)
+    errors = []
+
+    def work(t):
+        try:
+            for k in range(4):
+                b = (t * 4 + k) % n
+                assert_same(e.chunk_arrays(base[b * buf_len:(b + 1) * buf_len].tobytes()), exp[b], b)
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+
+
 def test_concurrent_callers_share_one_engine():
     """SparseDedupFile.eng is one static engine used by every flush thread (SparseDedupFile.java:100)."""
     e = engine_for(P())

@@ -127,3 +127,49 @@ def test_queue_4k_mean_mix_and_backup_buffers():
         st, ln, dg = out[i]
         assert st.tolist() == es.tolist() and ln.tolist() == el.tolist() and (dg == ed).all(), i
     b.destroy()
+
+
+@pytest.mark.parametrize("mix", [(4095, 0xFFF), (2047, 0x7FF)], ids=["default", "mix4k"])
+def test_early_completion_callers_leave_before_their_pass(mix):
+    """A pass's callers return as their own buffer's last chunk is fingerprinted (the kernel sets
+    the buffer's ready word in the pinned image), not when the pass's longest chunk is.  Passes
+    mixing buffers of maxLen-forced chunks (0x55 bytes: no boundary candidate at all, so every
+    chunk is a 32 KiB chain) with random buffers: every call's results are bit-exact, and calls
+    did complete early."""
+    prm = O.Params(min_len=mix[0], pred_mask=mix[1])
+    e = HipVariableSha256HashEngine(config=SdfsConfig(min_len=mix[0], pred_mask=mix[1]))
+    bufs = []
+    for i in range(96):
+        if i % 8 == 3:
+            b = np.full(L, 0x55, np.uint8)
+            b[:100] = O.synth(O.SYNTH_SEED, 9100 + i, 0, 100)
+        else:
+            b = O.synth(O.SYNTH_SEED, 9000 + i, 0, L)
+        bufs.append(b)
+    exp = [O.chunk(b.tobytes(), prm) for b in bufs]
+    e0 = e.queue_early()
+    errors = []
+
+    def work(t):
+        try:
+            for k in range(3):
+                i = (t * 3 + k) % len(bufs)
+                st, ln, dg = e.chunk_arrays(bufs[i].tobytes())
+                es, el, ed = exp[i]
+                assert st.tolist() == es.tolist() and ln.tolist() == el.tolist() and (dg == ed).all(), i
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(32)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:3]
+    # the C driver (no GIL between calls): the JNI glue's entry point at 48 threads
+    data = np.concatenate(bufs[:64])
+    r, res = T.getchunks(e, 48, data, L, 192, keep=True, mode="fill")
+    assert r.first_error == 0
+    _check(res, exp[:64], 64, 32)
+    assert e.queue_early() > e0
+    e.destroy()
