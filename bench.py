@@ -499,6 +499,7 @@ def main():
     ap.add_argument("--proxy-wgs", type=int, default=32, help="workgroups of the exchange proxy (RCCL channels)")
     ap.add_argument("--proxy-gbps", type=float, default=300.0, help="assumed per-GPU all-gather receive rate")
     ap.add_argument("--proxy-record-bytes", type=int, default=48, help="bytes per exchanged record")
+    ap.add_argument("--proxy-prio", type=int, default=0, help="1: the proxy's stream at high priority")
     args = ap.parse_args()
 
     launched = "WORLD_SIZE" in os.environ
@@ -606,17 +607,21 @@ def main():
         torch.cuda.synchronize()
         recs = int(batch.total.item())
         nb = ((args.exchange_proxy - 1) * recs * args.proxy_record_bytes + 15) // 16 * 16
-        proxy = [torch.cuda.Stream(device=device), torch.empty(nb, dtype=torch.uint8, device=device),
+        proxy = [torch.cuda.Stream(device=device, priority=-1 if args.proxy_prio else 0),
+                 torch.empty(nb, dtype=torch.uint8, device=device),
                  torch.zeros(nb, dtype=torch.uint8, device=device), nb]
-        # the proxy alone on the idle GPU: its own duration (the projected xGMI time)
+        # the proxy alone on the idle GPU (second launch: warm): its own duration, i.e. the
+        # projected xGMI time when the copy keeps its pace
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        proxy_after(proxy[0])
         e0.record(proxy[0])
         proxy_after(proxy[0])
         e1.record(proxy[0])
         e1.synchronize()
         proxy_info = {"ranks": args.exchange_proxy, "bytes_per_step": nb, "records_per_gpu_step": recs,
                       "record_bytes": args.proxy_record_bytes, "workgroups": args.proxy_wgs,
-                      "gbps": args.proxy_gbps, "alone_ms": round(e0.elapsed_time(e1), 4)}
+                      "gbps": args.proxy_gbps, "high_priority": bool(args.proxy_prio),
+                      "alone_ms": round(e0.elapsed_time(e1), 4)}
         for _ in range(2):
             step()
         torch.cuda.synchronize()

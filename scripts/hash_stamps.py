@@ -91,6 +91,8 @@ def main():
     res["stamped"] = st_run
     a = stamps.view(-1, 8).cpu().numpy().astype(np.uint64)
     a = a[a[:, 0] != 0]
+    if os.environ.get("STAMPS_OUT"):  # the raw per-wave stamps, for offline analysis
+        np.save(os.environ["STAMPS_OUT"], a[:, :6])
     r0, c0, r1, c1 = (a[:, k].astype(np.float64) for k in range(4))
     t0, t1 = r0.min(), r1.max()
     span_ms = (t1 - t0) / wall_mhz / 1e3

@@ -8,7 +8,7 @@ set -o pipefail
 O=gpurun_out/r6s1
 mkdir -p $O
 TL=$PWD/sdfs_amd/libsdfs_cdc_tuning.so
-Q="--steps 20 --warmup 3 --cpu-secs 0 --e2e-mib 0 --threads  --other-mix 0"
+Q="--steps 20 --warmup 3 --cpu-secs 0 --e2e-mib 0 --threads= --other-mix 0"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/pytest.log 2>&1 &&
 echo "pytest ok" &&
 timeout -k 10 120 python -u scripts/null_stream_probe.py r6 > $O/null_stream.jsonl 2> $O/null_stream.err &&

@@ -99,6 +99,7 @@ def test_bench_exchange_proxy_runs():
     _check_line(d)
     p = d["exchange_proxy"]
     assert p["ranks"] == 8 and p["bytes_per_step"] >= 7 * 48 * p["records_per_gpu_step"]
-    # paced at --proxy-gbps: alone it lasts about bytes / rate
+    # paced at --proxy-gbps: alone it lasts at least bytes / rate (longer only if its workgroups
+    # cannot copy that fast; the line reports the duration it had)
     want_ms = p["bytes_per_step"] / (p["gbps"] * 1e9) * 1e3
-    assert 0.8 * want_ms < p["alone_ms"] < 1.5 * want_ms, (p["alone_ms"], want_ms)
+    assert 0.8 * want_ms < p["alone_ms"] < 3.0 * want_ms, (p["alone_ms"], want_ms)

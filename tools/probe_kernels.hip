@@ -38,22 +38,28 @@ __global__ __launch_bounds__(256) void probe_sha256_kernel(uint32_t* sink, int b
     sink[blockIdx.x * 256 + threadIdx.x] = st[0] ^ st[1] ^ st[2] ^ st[3] ^ st[4] ^ st[5] ^ st[6] ^ st[7];
 }
 
-// Paced copy: workgroup g copies its contiguous share in 16 KiB pieces (256 lanes x 4 x 16 B), and
-// before each piece waits until the wall clock (s_memrealtime, `ticks_per_us` per microsecond)
-// reaches its own start + bytes done / the per-workgroup rate.
+// Paced copy: workgroup g copies its contiguous share in 32 KiB pieces (256 lanes x 8 x 16 B, all
+// loads of a piece in flight before its stores), and before each piece waits until the wall clock
+// (s_memrealtime) reaches its own start + bytes done / the per-workgroup rate.
 __global__ __launch_bounds__(256) void exchange_proxy_kernel(uint4* dst, const uint4* src, uint64_t n16,
                                                              double bytes_per_tick) {
     const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
     const uint64_t lo = (uint64_t)blockIdx.x * per;
     const uint64_t hi = lo + per < n16 ? lo + per : n16;
     const uint64_t t0 = wall_clock64();
-    for (uint64_t base = lo; base < hi; base += 1024) {
+    for (uint64_t base = lo; base < hi; base += 2048) {
         const uint64_t due = t0 + (uint64_t)((double)(base - lo) * 16.0 / bytes_per_tick);
         while (wall_clock64() < due) __builtin_amdgcn_s_sleep(8);
+        uint4 v[8];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < 8; k++) {
             const uint64_t i = base + k * 256 + threadIdx.x;
-            if (i < hi) dst[i] = src[i];
+            v[k] = i < hi ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint64_t i = base + k * 256 + threadIdx.x;
+            if (i < hi) dst[i] = v[k];
         }
     }
 }
