@@ -57,7 +57,9 @@ def sha_ceiling(local: int, waves_per_simd: int = 4) -> float:
     f = lib.sdfs_probe_sha256_ceiling
     f.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_double)] * 2
     g, ms = ctypes.c_double(), ctypes.c_double()
-    rc = f(local, waves_per_simd, 200, 5, ctypes.byref(g), ctypes.byref(ms))
+    # 2000 blocks per lane (~5 ms per launch): the launch's own ramp and drain stay well under 1 %
+    # (200 blocks made the ceiling ~3 % low: the fingerprint then appeared to beat it at 3 waves/SIMD)
+    rc = f(local, waves_per_simd, 2000, 3, ctypes.byref(g), ctypes.byref(ms))
     if rc:
         raise RuntimeError(f"sdfs_probe_sha256_ceiling failed: {rc}")
     return g.value
@@ -523,7 +525,8 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29533")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=torch.device(device))
+        from sdfs_amd.dist import exchange_pg_options
+        dist.init_process_group("nccl", device_id=torch.device(device), pg_options=exchange_pg_options())
 
     from sdfs_amd import HashFunctionPool, SdfsConfig
     from sdfs_amd.device import DeviceBatch

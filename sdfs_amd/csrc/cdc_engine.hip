@@ -162,8 +162,11 @@ constexpr int kEvPerRun = 2 * 8;
 constexpr uint32_t kSmall = 2 * kMaxBins + 8;  // hist | cursor | overflow, total, wave_ctr ..
 constexpr int kRing = 3;
 constexpr int kQueueInflight = 8;  // coalescing-queue lane streams (the most lanes a queue can run)
-constexpr int kQueueLanes = 4;     // lanes: batches on the device at once, one stream each (6 or 8
-                                   // measured no faster, profiles/r05/queue/lanes_cumask)
+constexpr int kQueueLanes = 6;     // lanes: batches on the device at once, one stream each.  Since
+                                   // callers leave as their own buffer is done (early completion), a
+                                   // pass's tail holds its lane with few callers left: 6 lanes at 48
+                                   // callers 12.5 -> 13.1 GiB/s (4 KiB mix), 9.3 -> 9.8 (default);
+                                   // 8 no better (profiles/r06/queue_early/)
 constexpr int kQueueSpareSlots = 4;  // slots beyond one per lane: the open one and the ones being read
 struct Workspace {
     DevBuf<uint32_t> bitmap;
@@ -261,7 +264,12 @@ struct DevEngine {
     uint32_t sec_log2 = 18;                  // section length of long buffers' cut walk (tuning: SDFS_SEC_LOG2)
     uint32_t skip_walk = 0;                  // measurement only (tuning: SDFS_SKIP_WALK 1..3): no chunks
     bool list_walk = true;                   // fused walk: LDS list form (tuning: SDFS_LIST_WALK=0 = queue walk)
-    bool scan_dyn = false;                   // scan work queue per wave (tuning: SDFS_SCAN_DYN=1; slower)
+    // Scan work handed out per wave from a counter instead of a static workgroup stride (tuning:
+    // SDFS_SCAN_DYN=0 = static): the same rate alone (interleaved A/B within 0.5 %), and a scan
+    // workgroup that starts late -- its CU held by another kernel, e.g. the exchange's RCCL
+    // all-gather at N > 1 -- no longer holds up the whole scan (one-GPU projection of the 8-rank
+    // exchange: +21 % per step with the static stride, +6-11 % with this; profiles/r06/exchange_proxy/)
+    bool scan_dyn = true;
     bool piece_walk = true;                  // sections walked in the scan's epilogue when they fit (tuning: SDFS_PIECE_WALK)
     bool scan_prio = false;                  // pre-fingerprint stages on a high-priority stream (tuning: SDFS_SCAN_PRIO)
     hipStream_t s_scan = nullptr;

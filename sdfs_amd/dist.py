@@ -24,6 +24,22 @@ import torch.distributed as dist
 RECORD_BYTES = 48
 
 
+def exchange_pg_options():
+    """ProcessGroupNCCL options for the exchange's process group: RCCL's internal stream at high
+    priority, so that its all-gather workgroups take CUs as soon as the chunking kernels free
+    them instead of queueing behind them.  One-GPU projection of the 8-rank exchange (bench.py
+    --exchange-proxy, profiles/r06/exchange_proxy/): +4 % per step instead of +21 % with the static
+    scan stride, +2.5 % instead of +6 % with the work-queue scan.  None where the backend has no
+    such options (gloo)."""
+    try:
+        from torch.distributed import ProcessGroupNCCL
+    except ImportError:
+        return None
+    o = ProcessGroupNCCL.Options()
+    o.is_high_priority_stream = True
+    return o
+
+
 def shard_streams(n_streams: int, world: int, rank: int) -> range:
     """Contiguous block of whole streams for `rank` (streams k*S/world .. (k+1)*S/world)."""
     lo = n_streams * rank // world
@@ -90,7 +106,7 @@ class RecordExchange:
         self.counts_host = [torch.zeros(self.world, dtype=torch.int64, pin_memory=self.cuda)
                             for _ in range(self.nslots)]
         self.counts_ev = [None] * self.nslots
-        self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        self.side = torch.cuda.Stream(self.device, priority=-1) if self.cuda else None
         self.pending = deque()  # slots submitted, table all-gather not issued yet (oldest first)
         self.results = []
         self.n = 0
@@ -281,7 +297,9 @@ class DeviceSetExchange:
                       for dv in self.devices]
         self.gathered = [[torch.empty(n * self.capacity, RECORD_BYTES, dtype=torch.uint8, device=dv) for _ in range(2)]
                          for dv in self.devices]
-        self.side = [torch.cuda.Stream(dv) for dv in self.devices]
+        # high priority: the exchange's RCCL workgroups take CUs as the chunking kernels free them
+        # (exchange_pg_options)
+        self.side = [torch.cuda.Stream(dv, priority=-1) for dv in self.devices]
         self.free = [[None] * slots for _ in self.devices]      # side-stream event: slot's exchange done
         self.prod = [[None] * slots for _ in self.devices]      # producer event: slot's table written
         self.totals = [[None] * slots for _ in self.devices]    # the step's device count tensor
