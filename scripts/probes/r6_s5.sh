@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 6, GPU session 5: latency-form workgroups spread one per CU (LDS padding) for queue passes,
+# A/B through the JNI fill entry at 1/8/48/128 callers, both mixes (tuning library).
+set -o pipefail
+O=gpurun_out/r6s5
+mkdir -p $O
+TL=$PWD/sdfs_amd/libsdfs_cdc_tuning.so
+for rep in 1 2; do
+  for mb in 12 11; do
+    for sp in 0 1; do
+      MASK_BITS=$mb MIN_SEG_KIB=$((mb == 12 ? 4 : 2)) MODE=fill THREADS=1,8,48,128 SDFS_CDC_LIB=$TL SDFS_SPLIT_SPREAD=$sp \
+        timeout -k 10 240 python -u scripts/queue_probe.py | sed "s/^{/{\"spread\": $sp, /" >> $O/queue_spread.jsonl 2>> $O/queue.err || exit 1
+    done
+    echo "rep $rep mix $mb ok"
+  done
+done

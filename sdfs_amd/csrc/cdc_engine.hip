@@ -167,6 +167,7 @@ constexpr int kQueueLanes = 6;     // lanes: batches on the device at once, one 
                                    // pass's tail holds its lane with few callers left: 6 lanes at 48
                                    // callers 12.5 -> 13.1 GiB/s (4 KiB mix), 9.3 -> 9.8 (default);
                                    // 8 no better (profiles/r06/queue_early/)
+constexpr uint32_t kSplitSpreadPad = 96 * 1024;  // + the kernel's 32 KiB: one per CU (160 KiB of LDS)
 constexpr int kQueueSpareSlots = 4;  // slots beyond one per lane: the open one and the ones being read
 struct Workspace {
     DevBuf<uint32_t> bitmap;
@@ -284,6 +285,7 @@ struct DevEngine {
     int fused_probe = 0;  // form (cdc_sweep_r3.hip launch_fused_probe)
     // latency form of the fingerprint: two lanes per chunk (tuning: SDFS_SPLIT_PACKED=0 = one lane)
     bool split_packed = true;
+    bool split_spread = false;  // one latency-form workgroup per CU for small passes (tuning: SDFS_SPLIT_SPREAD)
     // small-batch cut walk: candidate list + successors (tuning: SDFS_SMALL_BALLOT=1 = ballots only)
     bool small_ballot = false;
     hipEvent_t ev_front = nullptr;
@@ -755,7 +757,15 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
         // chunk's serial chain: the two-wave latency form shortens it
         if (e->hash_split && e->prm.hash_algo != SDFS_CDC_MD5 && e->hash_variant == 0 &&
             max_tasks <= (uint64_t)e->num_cus * 128)
-            HIP_TRY(launch_hash_split(ha, max_tasks, s, e->split_packed));
+        {
+            // A pass small enough for one latency-form workgroup per CU (the coalescing queue's)
+            // can pad its workgroups' LDS so that no two land on one CU: with several passes in
+            // flight (the queue's lanes) their serial chain waves would otherwise share SIMDs and
+            // issue at a fraction of a lone wave's rate (tuning: SDFS_SPLIT_SPREAD)
+            const uint64_t groups = (max_tasks + 31) / 32;
+            const uint32_t pad = e->split_spread && groups <= (uint64_t)e->num_cus ? kSplitSpreadPad : 0u;
+            HIP_TRY(launch_hash_split(ha, max_tasks, s, e->split_packed, pad));
+        }
 #ifdef SDFS_TUNING
         else if (e->fused_probe && fused && nbuf >= (uint32_t)e->num_cus * 4)
             HIP_TRY(launch_fused_probe(sa, ha, w->small.p + 2 * kMaxBins + 4, (int)e->prm.window, pk, e->num_cus,
@@ -1429,6 +1439,7 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_FRONT_SERIAL")) e->front_serial = atoi(v) != 0;
     if (const char* v = getenv("SDFS_FUSED_PROBE")) e->fused_probe = atoi(v);
     if (const char* v = getenv("SDFS_SPLIT_PACKED")) e->split_packed = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SPLIT_SPREAD")) e->split_spread = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SMALL_BALLOT")) e->small_ballot = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;

@@ -220,7 +220,8 @@ hipError_t launch_prefix(const PrefixArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, hipStream_t stream);
 hipError_t launch_hash(const HashArgs& a, uint64_t max_tasks, int variant, hipStream_t stream, bool packed = true);
 // latency form for small batches (SHA-256 / SHA-256/160 only): two waves per 64 chunks
-hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t stream, bool packed = true);
+hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t stream, bool packed = true,
+                             uint32_t lds_pad = 0);
 hipError_t launch_extent_order(const ExtentArgs& a, hipStream_t stream);
 hipError_t launch_copy_out(const void* src, void* dst, uint64_t bytes, hipStream_t stream);
 // Early completion (HashArgs::done_ctr): everything the pinned image's header needs before the
