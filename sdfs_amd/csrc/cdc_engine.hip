@@ -1307,6 +1307,7 @@ bool queue_ready(DevEngine* e) {
 #ifdef SDFS_TUNING
     if (const char* v = getenv("SDFS_Q_INFLIGHT")) c.lanes = std::max(1, std::min(atoi(v), kQueueInflight));
     if (const char* v = getenv("SDFS_Q_LINGER_US")) c.linger_us = (uint32_t)atoi(v);
+    if (const char* v = getenv("SDFS_Q_SHARE_DIV")) c.share_div = (uint32_t)std::max(1, atoi(v));
 #endif
     c.nslots = c.lanes + kQueueSpareSlots;
     c.max_reqs = 1024;

@@ -205,6 +205,7 @@ class CoalescingQueue {
         uint64_t max_req_bytes = 0;  // larger requests bypass the queue (0 = cap / 2)
         uint32_t linger_us = 250;  // longest a request waits for company while a batch is in flight
         uint32_t poll_us = 10;     // early completion (Backend::poll): the completer's poll period
+        uint32_t share_div = 1;    // a slot goes once it holds active callers / (lanes x share_div)
     };
 
     CoalescingQueue(Backend& b, Config c)
@@ -446,7 +447,8 @@ class CoalescingQueue {
         const size_t n = o.nreq();
         if (n == 0) return false;
         if (stop_) return true;  // draining: launch what was placed
-        const size_t share = (size_t)((active_ + c_.lanes - 1) / c_.lanes);
+        const size_t lanes = (size_t)c_.lanes * (c_.share_div ? c_.share_div : 1);
+        const size_t share = ((size_t)active_ + lanes - 1) / lanes;
         if (inflight_ == 0 || o.full || n >= share) return true;
         *deadline = o.t_open + std::chrono::microseconds(c_.linger_us);
         return std::chrono::steady_clock::now() >= *deadline;
