@@ -136,6 +136,21 @@ def table_digest(torch, rows) -> str:
     return hashlib.sha256(rows.contiguous().cpu().numpy().tobytes()).hexdigest()
 
 
+def exchange_check(torch, dist, gathered, counts, own_slot, total, rank, world, device) -> dict:
+    """Self-check of one exchanged step (collective: every rank calls it): every rank's count equals
+    its batch's chunk total, and this rank's rows of the gathered table (rank r's rows at
+    [r * max, r * max + counts[r])) are the records its engine wrote into its slot."""
+    mx = max(counts)
+    mine = gathered[rank * mx: rank * mx + counts[rank]]
+    tot = torch.tensor([total], device=device, dtype=torch.int64)
+    tots = [torch.zeros_like(tot) for _ in range(world)]
+    dist.all_gather(tots, tot)
+    tots = [int(x.item()) for x in tots]
+    return {"counts": list(counts), "stride": mx, "counts_match": list(counts) == tots,
+            "rows_match": bool(torch.equal(mine, own_slot[: counts[rank]])),
+            "table_sha256": [table_digest(torch, mine)] if rank == 0 else None}
+
+
 def cpu_baseline_block(args, cfg):
     aff = len(os.sched_getaffinity(0))
     quota = cpu_quota()
@@ -660,15 +675,7 @@ def main():
     ex_check = None
     if ex is not None and last_exchange:
         (gathered, cl), k_last = last_exchange
-        mx = max(cl)
-        mine = gathered[rank * mx: rank * mx + cl[rank]]
-        tot = torch.tensor([total], device=device, dtype=torch.int64)
-        tots = [torch.zeros_like(tot) for _ in range(world)]
-        dist.all_gather(tots, tot)
-        tots = [int(x.item()) for x in tots]
-        ex_check = {"counts": cl, "stride": mx, "counts_match": cl == tots,
-                    "rows_match": bool(torch.equal(mine, ex.slots[k_last][: cl[rank]])),
-                    "table_sha256": [table_digest(torch, mine)] if rank == 0 else None}
+        ex_check = exchange_check(torch, dist, gathered, cl, ex.slots[k_last], total, rank, world, device)
 
     # The roofline's launch duration: chunk_hash timed with HIP events over a one-stream timed
     # region (every step stream-ordered, so no other kernel shares the GPU with chunk_hash and its

@@ -277,3 +277,57 @@ def test_configs3_chunked_records_exchange_gloo(world):
             assert st == cover.get(bid, 0)
             cover[bid] = st + ln
         assert cover == {b: _BL for b in range(world * nbuf)}
+
+
+def _check_worker(rank, world, port, q):
+    """bench.py's exchange self-check over a pipelined RecordExchange (direct slots), as the
+    torchrun form at N > 1 runs it, with one rank's count deliberately off on the last step."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cap = 64
+        ex = RecordExchange(cap, "cpu", depth=2, slots=3)
+        ex.direct = True
+        last = None
+        for step in range(5):
+            n = 10 + 3 * rank + step
+            slot = ex.acquire()
+            slot[:n] = (rank * 40 + step) % 256
+            slot[n:] = 0xEE
+            ex.submit(slot, torch.tensor([n]))
+            last = (n, (ex.n - 1) % ex.nslots)
+        res = ex.flush()
+        (gathered, cl), k_last = res[-1], last[1]
+        good = bench.exchange_check(torch, dist, gathered, cl, ex.slots[k_last], last[0], rank, world, "cpu")
+        bad = bench.exchange_check(torch, dist, gathered, cl, ex.slots[k_last], last[0] + (rank == 1), rank, world, "cpu")
+        q.put((rank, good, bad))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_exchange_check_gloo(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_check_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, good, bad = q.get(timeout=180)
+        res[r] = (good, bad)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r, (good, bad) in res.items():
+        assert good["counts"] == [10 + 3 * k + 4 for k in range(world)]
+        assert good["counts_match"] and good["rows_match"]
+        assert good["stride"] == max(good["counts"])
+        assert (good["table_sha256"] is not None) == (r == 0)
+        assert not bad["counts_match"] and bad["rows_match"]
