@@ -1188,6 +1188,7 @@ struct sdfs_cdc_lz4 {
     int lane_mode = -1;           // -1 auto (hybrid from kHybridChunksPerCu chunks per CU up), 0 wave
                                   // kernel, 1 lane kernel only, 2 hybrid (SDFS_LZ4_LANE, tuning build)
     int lane_wg_per_cu = 4;       // SDFS_LZ4_LANE_WG_PER_CU: 256-thread workgroups per CU (lane mode)
+    int lane_grid = 0;            // SDFS_LZ4_LANE_GRID: at most this many lane workgroups (0 = no cap)
     ZBuf<uint32_t> ltag;
     ZBuf<uint32_t> bail;          // hybrid (lane_mode 2): count + bailed chunk indices
     int screen = 1;               // literal screen before the exact kernels (SDFS_LZ4_SCREEN=0: off, tuning build)
@@ -1306,7 +1307,8 @@ int launch_compress_impl(sdfs_cdc_lz4* z, const Lz4Args& a0, hipStream_t s) {
     // n_max bounds a device-count batch, so the choice follows the capacity the caller gives.
     const int lane_mode = z->lane_mode >= 0 ? z->lane_mode
                                             : (a.n_max >= (uint64_t)z->num_cus * kHybridChunksPerCu ? 2 : 0);
-    const uint64_t lgrid = std::min<uint64_t>((a.n_max + 255) / 256, (uint64_t)z->num_cus * z->lane_wg_per_cu);
+    uint64_t lgrid = std::min<uint64_t>((a.n_max + 255) / 256, (uint64_t)z->num_cus * z->lane_wg_per_cu);
+    if (z->lane_grid > 0) lgrid = std::min<uint64_t>(lgrid, (uint64_t)z->lane_grid);  // tuning: fewer chains
     if (lane_mode == 1 && !lane_tables(z, lgrid * 256, s))
         return fail_status(SDFS_CDC_EHIP, "lz4: cannot allocate %llu lane tables", (unsigned long long)(lgrid * 256));
     if (lane_mode == 1 || (lane_mode == 2 && lane_tables(z, lgrid * 256, s))) {
@@ -1406,6 +1408,7 @@ int sdfs_cdc_lz4_create(int device, int mode, sdfs_cdc_lz4** out) {
     if (const char* v = getenv("SDFS_LZ4_WG_PER_CU")) z->wg_per_cu = std::max(1, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_LANE")) z->lane_mode = atoi(v);
     if (const char* v = getenv("SDFS_LZ4_LANE_WG_PER_CU")) z->lane_wg_per_cu = std::max(1, atoi(v));
+    if (const char* v = getenv("SDFS_LZ4_LANE_GRID")) z->lane_grid = std::max(0, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_BAIL")) z->bail_misses = (uint32_t)std::max(0, atoi(v));
     if (const char* v = getenv("SDFS_LZ4_LANE_SORT")) z->lane_sort = atoi(v);
     if (const char* v = getenv("SDFS_LZ4_LANE_DEPTH")) z->lane_depth = atoi(v);
