@@ -73,8 +73,9 @@ def test_bench_device_set_form_n1():
     assert len(d["kernels_ms"]["chunk_hash_per_gpu"]) == 1 and d["one_stream"]["value"] > 0
     plain = _plain()
     assert ex["table_sha256"][0] == plain["records_sha256"] == d["records_sha256"]
-    # the device-set line is the same work as the headline: within 10 % of it on one box
-    assert d["value"] > 0.9 * plain["value"], (d["value"], plain["value"])
+    # the device-set line is the same work as the headline (3 steps here, so only a loose bound:
+    # the full-length lines are 3.5 % apart, profiles/r06/bench/)
+    assert d["value"] > 0.8 * plain["value"], (d["value"], plain["value"])
 
 
 @pytest.mark.gpu
