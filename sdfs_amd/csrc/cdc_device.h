@@ -1855,9 +1855,11 @@ __device__ __forceinline__ uint32_t pair_swap(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);
 }
 
-template <int ALGO>
+// BYBUF: base = the group's first chunk index within buffer `bb`, ntask = that buffer's count,
+// and the chunks are taken in slot order (no task list)
+template <int ALGO, bool BYBUF = false>
 __device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint32_t base, uint32_t ntask,
-                                                        uint32_t wave, uint4 (&wk)[2][16][64]) {
+                                                        uint32_t wave, uint4 (&wk)[2][16][64], uint32_t bb = 0) {
     static_assert(ALGO != 2, "MD5 has no split form");
     const uint32_t lane = threadIdx.x & 63;
     const bool producer = wave == 0, consumer = wave == 1;
@@ -1868,9 +1870,15 @@ __device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint3
     uint32_t slot = 0, b = 0, kk = 0, cs = 0, len = 0, nfull = 0, nblocks = 0;
     const uint8_t* p = a.zero_page;
     if (valid) {
-        slot = a.tasks[i];
-        b = slot / a.cap;
-        kk = slot - b * a.cap;
+        if constexpr (BYBUF) {
+            b = bb;
+            kk = i;
+            slot = bb * a.cap + i;
+        } else {
+            slot = a.tasks[i];
+            b = slot / a.cap;
+            kk = slot - b * a.cap;
+        }
         const uint64_t boff = a.uniform_len ? (uint64_t)b * a.uniform_len : a.offs[b];
         cs = a.starts[slot];
         len = a.clens[slot];
@@ -1879,6 +1887,11 @@ __device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint3
         nblocks = (len + 8) / 64 + 1;
     }
     const uint32_t maxnb = wave_max_u32(nblocks);  // identical in both waves (same 32 tasks)
+#ifdef SDFS_TUNING
+    const bool masked = a.split_masked != 0;  // A/B: the round-6 form, finished lanes masked off
+#else
+    constexpr bool masked = false;
+#endif
     if (producer) {
         // the A lanes' W + K: zero, once for both buffers
 #pragma unroll
@@ -1898,6 +1911,12 @@ __device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint3
              x2 = elane ? 0x1f83d9abu : 0x3c6ef372u, x3 = elane ? 0x5be0cd19u : 0xa54ff53au;
     uint4 nx[4];
     if (producer) load_block64(nx, nfull ? p : a.zero_page);
+#ifdef SDFS_TUNING
+    // measurement (scripts/split_stamps.py): shader clock at start and end, the cycles this wave
+    // spent in the per-block barrier, and where it ran
+    const uint64_t st_c0 = clock64(), st_r0 = wall_clock64();
+    uint64_t st_wait = 0, st_mid = 0;
+#endif
     for (uint32_t it = 0; it <= maxnb; it++) {
         if (producer) {
             if (it < maxnb) {
@@ -1906,7 +1925,9 @@ __device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint3
 #pragma unroll
                 for (int q = 0; q < 4; q++) cur[q] = nx[q];
                 load_block64(nx, blk + 1 < nfull ? p + 64 * (blk + 1) : a.zero_page);
-                if (valid && blk < nblocks) {
+                // every producer lane with a chunk slot runs the schedule (a finished or empty
+                // slot on zeros: its consumer lanes discard the block), see the consumer below
+                if (k < (uint32_t)kSplitTasksPacked && (!masked || (valid && blk < nblocks))) {
                     uint32_t w[16];
                     if (blk < nfull) {
 #pragma unroll
@@ -1950,7 +1971,11 @@ __device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint3
             }
         } else if (consumer && it >= 1) {
             const uint32_t blk = it - 1;
-            if (valid && blk < nblocks) {  // the same for both lanes of a chunk
+            // Every lane runs every block and a lane whose chunk is done (or that has none) keeps
+            // its state: a wave with lanes masked off ran its blocks up to 1.6x slower (stamps,
+            // scripts/split_stamps.py), which put a pass's longest chunk on its slowest path.
+            const bool act = valid && blk < nblocks;  // the same for both lanes of a chunk
+            if (act || !masked) {
                 const uint4(*src)[64] = wk[blk & 1];
                 const uint32_t s0 = x0, s1 = x1, s2 = x2, s3 = x3;
                 uint4 q = src[0][lane];
@@ -1977,14 +2002,38 @@ __device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint3
                     }
                     q = qn;
                 }
-                x0 += s0;
-                x1 += s1;
-                x2 += s2;
-                x3 += s3;
+                const uint32_t m = act ? ~0u : 0u;
+                x0 = s0 + (x0 & m);
+                x1 = s1 + (x1 & m);
+                x2 = s2 + (x2 & m);
+                x3 = s3 + (x3 & m);
             }
         }
+#ifdef SDFS_TUNING
+        const uint64_t st_b = clock64();
         __syncthreads();
+        st_wait += clock64() - st_b;
+        if (it == 32) st_mid = clock64();
+#else
+        __syncthreads();
+#endif
     }
+#ifdef SDFS_TUNING
+    if (a.stamps && lane == 0) {
+        const uint64_t c1 = clock64(), r1 = wall_clock64();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);    // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID
+        uint64_t* st = a.stamps + 8ull * (2 * blockIdx.x + wave);
+        st[0] = st_r0;
+        st[1] = st_c0;
+        st[2] = r1;
+        st[3] = c1;
+        st[4] = (uint64_t)xcc << 32 | hw;
+        st[5] = maxnb | (uint64_t)(1 + wave) << 32;
+        st[6] = st_wait;
+        st[7] = st_mid;
+    }
+#endif
     // e..h from the E lane, stored by the A lane
     const uint32_t e4 = pair_swap(x0), e5 = pair_swap(x1), e6 = pair_swap(x2), e7 = pair_swap(x3);
     if (consumer && valid && !elane) {
@@ -1996,6 +2045,15 @@ __device__ __forceinline__ void hash_split_group_packed(const HashArgs& a, uint3
 template <int ALGO>
 __global__ __launch_bounds__(128) void chunk_hash_split_packed_kernel(HashArgs a) {
     __shared__ uint4 wk[2][16][64];  // [buffer][t / 4][consumer lane]: odd = W[t..t+3] + K[t..t+3], even = 0
+    if (a.bybuf) {
+        // workgroup b * bybuf + g: chunks 32g .. 32g+31 of buffer b (all groups of a pass run at
+        // once, so each buffer is done after its own longest chunk)
+        const uint32_t b = blockIdx.x / a.bybuf, base = (blockIdx.x - b * a.bybuf) * kSplitTasksPacked;
+        const uint32_t n = min(a.counts[b], a.cap);
+        if (base >= n) return;  // uniform
+        hash_split_group_packed<ALGO, true>(a, base, n, threadIdx.x >> 6, wk, b);
+        return;
+    }
     const uint32_t ntask = *a.total;
     if (blockIdx.x * kSplitTasksPacked >= ntask) return;  // whole workgroup past the end (uniform)
     hash_split_group_packed<ALGO>(a, blockIdx.x * kSplitTasksPacked, ntask, threadIdx.x >> 6, wk);

@@ -286,6 +286,9 @@ struct DevEngine {
     // latency form of the fingerprint: two lanes per chunk (tuning: SDFS_SPLIT_PACKED=0 = one lane)
     bool split_packed = true;
     bool split_spread = false;  // one latency-form workgroup per CU for small passes (tuning: SDFS_SPLIT_SPREAD)
+    bool split_masked = false;  // tuning: SDFS_SPLIT_MASKED (latency form, finished lanes masked off)
+    bool split_bybuf = false;   // latency-form groups per buffer, not per 32 longest (tuning: SDFS_SPLIT_BYBUF;
+                                // measured slower)
     // small-batch cut walk: candidate list + successors (tuning: SDFS_SMALL_BALLOT=1 = ballots only)
     bool small_ballot = false;
     hipEvent_t ev_front = nullptr;
@@ -764,6 +767,14 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
             // issue at a fraction of a lone wave's rate (tuning: SDFS_SPLIT_SPREAD)
             const uint64_t groups = (max_tasks + 31) / 32;
             const uint32_t pad = e->split_spread && groups <= (uint64_t)e->num_cus ? kSplitSpreadPad : 0u;
+            // groups drawn from one buffer would end that buffer with its own longest chunk
+            // instead of the group holding the pass's 32 longest — but they put more long chains
+            // side by side on the SIMDs, and measured slower at 1-128 callers
+            ha.split_masked = e->split_masked;
+            if (e->split_bybuf && e->split_packed) {
+                ha.bybuf = (out->cap + 31) / 32;
+                ha.counts = out->counts;
+            }
             HIP_TRY(launch_hash_split(ha, max_tasks, s, e->split_packed, pad));
         }
 #ifdef SDFS_TUNING
@@ -1441,6 +1452,8 @@ int dev_create(const sdfs_cdc_params* p, int ordinal, std::unique_ptr<DevEngine>
     if (const char* v = getenv("SDFS_FUSED_PROBE")) e->fused_probe = atoi(v);
     if (const char* v = getenv("SDFS_SPLIT_PACKED")) e->split_packed = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SPLIT_SPREAD")) e->split_spread = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SPLIT_BYBUF")) e->split_bybuf = atoi(v) != 0;
+    if (const char* v = getenv("SDFS_SPLIT_MASKED")) e->split_masked = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SMALL_BALLOT")) e->small_ballot = atoi(v) != 0;
     if (const char* v = getenv("SDFS_SCAN_MAX_BLOCK"))
         e->scan_max_block = (uint32_t)std::max(256, std::min(atoi(v), kScanThreads)) / 256 * 256;

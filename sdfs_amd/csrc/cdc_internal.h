@@ -177,6 +177,12 @@ struct HashArgs {
     const uint32_t* counts;
     uint32_t* ready;
     uint32_t seq;
+    // Per-buffer groups of the latency form (chunk_hash_split_packed_kernel): > 0 = workgroup
+    // b * bybuf + g takes chunks 32g .. 32g+31 of buffer b in slot order (`counts` required),
+    // so a buffer's fingerprints end with its own longest chunk, not the pass's; 0 = groups of
+    // the longest-first task list
+    uint32_t bybuf;
+    uint32_t split_masked;     // tuning A/B only (SDFS_SPLIT_MASKED): latency form with finished lanes masked off
     // measurement only (tuning build, fingerprint variant 50): per wave {wall clock, shader clock}
     // at its start and end, and its HW_ID / XCC_ID, 8 u64 per wave (scripts/hash_stamps.py)
     uint64_t* stamps;

@@ -995,7 +995,9 @@ hipError_t launch_hash_split(const HashArgs& a, uint64_t max_tasks, hipStream_t 
         // production: two lanes per chunk on the chain (11 instead of 14 instructions per round).
         // lds_pad: dynamic LDS no lane touches, so that at most one such workgroup fits a CU and
         // its chain wave does not share a SIMD with another pass's (the caller decides when)
-        const uint32_t blocks = (uint32_t)((max_tasks + kSplitTasksPacked - 1) / kSplitTasksPacked);
+        // bybuf: max_tasks = nbuf * cap, one group per 32 slots of each buffer
+        const uint32_t blocks = a.bybuf ? (uint32_t)(max_tasks / a.cap) * a.bybuf
+                                        : (uint32_t)((max_tasks + kSplitTasksPacked - 1) / kSplitTasksPacked);
         if (blocks == 0) return hipSuccess;
         switch (a.algo) {
         case 0: hipLaunchKernelGGL((chunk_hash_split_packed_kernel<0>), dim3(blocks), dim3(128), lds_pad, s, a); break;
