@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 6, GPU session 19: host CPU per getChunks call (callers / queue threads / runtime) at
+# 1/8/48/128 callers, both mixes, production library, 150 calls per thread.
+set -o pipefail
+O=gpurun_out/r6s19
+mkdir -p $O
+for mb in 12 11; do
+  MASK_BITS=$mb MIN_SEG_KIB=$((mb == 12 ? 4 : 2)) MODE=fill THREADS=1,8,48,128 CALLS_PER_THREAD=150 \
+    timeout -k 10 300 python -u scripts/queue_probe.py >> $O/cpu.jsonl 2>> $O/err.log || exit 1
+done
+cat $O/cpu.jsonl

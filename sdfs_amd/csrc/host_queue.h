@@ -209,7 +209,7 @@ class CoalescingQueue {
     };
 
     CoalescingQueue(Backend& b, Config c)
-        : b_(b), c_(c), slots_(c.nslots), done_cv_(c.nslots), flight_(c.lanes), comp_cv_(c.lanes),
+        : b_(b), c_(c), slots_(c.nslots), flight_(c.lanes), comp_cv_(c.lanes),
           lane_busy_(c.lanes, 0), early_(c.lanes) {}
     ~CoalescingQueue() { shutdown(); }
     CoalescingQueue(const CoalescingQueue&) = delete;
@@ -320,7 +320,7 @@ class CoalescingQueue {
         const int frc = fill(s->in + r.off);
         lk.lock();
         if (--s->copying == 0) cv_disp_.notify_all();
-        done_cv_[r.slot].wait(lk, [&] { return r.done; });  // woken with its own slot only
+        done_cv(&r).wait(lk, [&] { return r.done; });  // woken with its own request (about) only
         lk.unlock();
         const int ret = frc ? frc : read(*s, r, r.status);
         lk.lock();
@@ -364,9 +364,14 @@ class CoalescingQueue {
         if (--active_ == 0 && stop_) idle_cv_.notify_all();
     }
 
-    std::condition_variable& admit_cv(const QReq* q) {
-        return cv_admit_[(reinterpret_cast<uintptr_t>(q) >> 6) % kAdmitCvs];
+    // Condition variables picked by a request's address (Fibonacci hashing: requests live on their
+    // callers' stacks, which sit at the same offset in equally sized stacks, so low address bits
+    // alone would put every caller on one variable)
+    static size_t cv_index(const QReq* q, size_t n) {
+        return (size_t)((reinterpret_cast<uintptr_t>(q) * 0x9E3779B97F4A7C15ull) >> 40) % n;
     }
+    std::condition_variable& admit_cv(const QReq* q) { return cv_admit_[cv_index(q, kAdmitCvs)]; }
+    std::condition_variable& done_cv(const QReq* q) { return cv_done_[cv_index(q, kDoneCvs)]; }
 
     // Places `r` in the open slot, opening a free slot when there is none (queue lock held).
     // 1 = placed (the caller copies its bytes to s.in + r.off next), 0 = no room now (the open
@@ -455,6 +460,9 @@ class CoalescingQueue {
     }
 
     void dispatcher() {
+#ifdef __linux__
+        prctl(PR_SET_NAME, "sdfs-qdisp", 0, 0, 0);  // per-thread CPU accounting (scripts/queue_probe.py)
+#endif
         std::unique_lock<std::mutex> lk(m_);
         for (;;) {
             std::chrono::steady_clock::time_point deadline{};
@@ -505,7 +513,6 @@ class CoalescingQueue {
     int wait_early(QSlot& s, int lane, std::unique_lock<std::mutex>& lk) {
         std::vector<uint8_t>& rdy = early_[lane];
         rdy.assign(s.chunks.size(), 0);  // the slot is closed: its request list does not change
-        const int idx = (int)(&s - slots_.data());
         size_t left = s.chunks.size();
         for (;;) {
             bool fin = false;
@@ -519,13 +526,11 @@ class CoalescingQueue {
                     rdy[i] = 2;  // completed early: the request may be gone once its caller wakes
                     s.chunks[i]->status = 0;
                     s.chunks[i]->done = true;
+                    done_cv(s.chunks[i]).notify_all();  // lock held: the request is still there
                     early_done_++;
                     left--;
                 }
-            if (any) {
-                done_cv_[idx].notify_all();
-                lk.unlock();
-            }
+            if (any) lk.unlock();
             if (left == 0) return b_.wait(s);  // nothing else can complete early
             std::this_thread::sleep_for(std::chrono::microseconds(c_.poll_us));
         }
@@ -535,6 +540,7 @@ class CoalescingQueue {
     void completer(int lane) {
 #ifdef __linux__
         prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us: the poll period's sleeps stay short
+        prctl(PR_SET_NAME, "sdfs-qcomp", 0, 0, 0);
 #endif
         std::unique_lock<std::mutex> lk(m_);
         for (;;) {
@@ -566,12 +572,13 @@ class CoalescingQueue {
                 if (polled && early_[lane][i] == 2) continue;  // completed (and maybe gone) already
                 s->chunks[i]->status = s->status;
                 s->chunks[i]->done = true;
+                done_cv(s->chunks[i]).notify_all();
             }
             for (QReq* q : s->hashes) {
                 q->status = s->status;
                 q->done = true;
+                done_cv(q).notify_all();
             }
-            done_cv_[s - slots_.data()].notify_all();
             if (s->readers == 0) {  // every caller completed early and has left
                 s->state = QSlot::kFree;
                 admit_waiting();
@@ -592,7 +599,11 @@ class CoalescingQueue {
     std::deque<QReq*> waitq_;
     std::condition_variable cv_admit_[kAdmitCvs];
     std::condition_variable cv_disp_;
-    std::vector<std::condition_variable> done_cv_;  // per slot: its callers wait for its batch
+    // a caller waits for its request's completion on one of these (done_cv): completing a request
+    // wakes about one thread, not every caller of the pass (round 6: with early completion a pass
+    // of 30 callers woke all 30 up to ~10 times, ~200 us of CPU per call at 128 callers)
+    static constexpr size_t kDoneCvs = 256;
+    std::condition_variable cv_done_[kDoneCvs];
     std::vector<std::deque<QSlot*>> flight_;        // per lane, in launch order
     std::vector<std::condition_variable> comp_cv_;  // per lane
     std::vector<int> lane_busy_;

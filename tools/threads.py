@@ -17,7 +17,8 @@ LIB_TUNING = os.path.join(HERE, "libsdfs_threads_tuning.so")
 class Result(ctypes.Structure):
     _fields_ = [("secs", ctypes.c_double), ("gibps", ctypes.c_double), ("mean_us", ctypes.c_double),
                 ("p50_us", ctypes.c_double), ("p90_us", ctypes.c_double), ("p99_us", ctypes.c_double),
-                ("max_us", ctypes.c_double), ("calls", ctypes.c_uint64), ("first_error", ctypes.c_int)]
+                ("max_us", ctypes.c_double), ("calls", ctypes.c_uint64), ("first_error", ctypes.c_int),
+                ("caller_cpu_us", ctypes.c_double), ("fill_us", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {k: (round(getattr(self, k), 3) if isinstance(getattr(self, k), float) else getattr(self, k))

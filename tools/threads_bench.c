@@ -23,6 +23,8 @@ typedef struct sdfs_threads_result {
     double mean_us, p50_us, p90_us, p99_us, max_us;
     uint64_t calls;
     int first_error;  /* 0 or the first non-zero status */
+    double caller_cpu_us; /* CPU time of the calling threads over their calls (CLOCK_THREAD_CPUTIME_ID) */
+    double fill_us;       /* wall time the calling threads spent in the fill callback (mode 1) */
 } sdfs_threads_result;
 
 typedef struct {
@@ -45,6 +47,7 @@ typedef struct {
     struct gate* gate;
     int err;
     struct timespec end;
+    double cpu_us, fill_us;
 } worker_t;
 
 /* start gate: every worker waits until all have been created, then they start together */
@@ -64,8 +67,18 @@ static double ts_us(const struct timespec* a, const struct timespec* b) {
     return (double)(b->tv_sec - a->tv_sec) * 1e6 + (double)(b->tv_nsec - a->tv_nsec) / 1e3;
 }
 
+struct fill_ctx {
+    const uint8_t* src;
+    double* acc_us;
+};
+
 static int copy_fill(void* ctx, uint8_t* dst, uint32_t len) {
-    memcpy(dst, ctx, len);
+    const struct fill_ctx* f = (const struct fill_ctx*)ctx;
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    memcpy(dst, f->src, len);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    *f->acc_us += (double)(b.tv_sec - a.tv_sec) * 1e6 + (double)(b.tv_nsec - a.tv_nsec) / 1e3;
     return 0;
 }
 
@@ -76,6 +89,8 @@ static void* worker(void* arg) {
     uint32_t* ln = malloc(sizeof(uint32_t) * w->cap);
     uint8_t* dg = malloc((size_t)w->cap * 32);
     gate_wait(w->gate);
+    struct timespec c0, c1;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
     for (uint64_t i = (uint64_t)w->tid; i < w->total_calls; i += (uint64_t)w->nthreads) {
         const uint64_t b = i % w->nbuf;
         const uint8_t* buf = w->data + b * w->buf_len;
@@ -87,9 +102,11 @@ static void* worker(void* arg) {
             uint32_t* so = w->counts ? w->starts + b * w->cap : st;
             uint32_t* lo = w->counts ? w->lens + b * w->cap : ln;
             uint8_t* dgo = w->counts ? w->digests + b * w->cap * (uint64_t)dl : dg;
-            if (w->mode == 1)
-                rc = sdfs_cdc_get_chunks_fill(w->e, SDFS_CDC_NO_STREAM, w->buf_len, copy_fill, (void*)buf, so, lo, dgo,
+            if (w->mode == 1) {
+                struct fill_ctx f = {buf, &w->fill_us};
+                rc = sdfs_cdc_get_chunks_fill(w->e, SDFS_CDC_NO_STREAM, w->buf_len, copy_fill, &f, so, lo, dgo,
                                               w->cap, &n);
+            }
             else if (w->mode == 2)
                 rc = sdfs_cdc_get_chunks_stream(w->e, b / 16, buf, w->buf_len, so, lo, dgo, w->cap, &n);
             else
@@ -103,6 +120,8 @@ static void* worker(void* arg) {
         if (rc && !w->err) w->err = rc;
     }
     clock_gettime(CLOCK_MONOTONIC, &w->end);
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
+    w->cpu_us = ts_us(&c0, &c1);
     free(st);
     free(ln);
     free(dg);
@@ -118,6 +137,7 @@ static int run(sdfs_cdc_engine* const* hs, int nh, int kind, int mode, int nthre
                uint32_t buf_len, uint64_t total_calls, uint32_t cap, uint32_t* counts, uint32_t* starts,
                uint32_t* lens, uint8_t* digests, sdfs_threads_result* res) {
     if (!hs || nh < 1 || !data || nthreads < 1 || nbuf == 0 || !res || total_calls == 0) return -1;
+    res->caller_cpu_us = res->fill_us = 0;
     worker_t* ws = calloc((size_t)nthreads, sizeof(worker_t));
     pthread_t* th = calloc((size_t)nthreads, sizeof(pthread_t));
     double* lat = calloc(total_calls, sizeof(double));
@@ -169,6 +189,8 @@ static int run(sdfs_cdc_engine* const* hs, int nh, int kind, int mode, int nthre
         if (ws[t].end.tv_sec > end.tv_sec || (ws[t].end.tv_sec == end.tv_sec && ws[t].end.tv_nsec > end.tv_nsec))
             end = ws[t].end;
         if (ws[t].err && !res->first_error) res->first_error = ws[t].err;
+        res->caller_cpu_us += ws[t].cpu_us;
+        res->fill_us += ws[t].fill_us;
     }
     double sum = 0;
     for (uint64_t i = 0; i < total_calls; i++) sum += lat[i];
