@@ -210,7 +210,7 @@ class CoalescingQueue {
 
     CoalescingQueue(Backend& b, Config c)
         : b_(b), c_(c), slots_(c.nslots), flight_(c.lanes), comp_cv_(c.lanes),
-          lane_busy_(c.lanes, 0), early_(c.lanes) {}
+          lane_busy_(c.lanes, 0), early_(c.lanes), wake_(c.lanes) {}
     ~CoalescingQueue() { shutdown(); }
     CoalescingQueue(const CoalescingQueue&) = delete;
     CoalescingQueue& operator=(const CoalescingQueue&) = delete;
@@ -315,8 +315,8 @@ class CoalescingQueue {
             return kQueueTooBig;
         }
         QSlot* s = &slots_[r.slot];
-        cv_disp_.notify_one();
         lk.unlock();
+        cv_disp_.notify_one();  // after the unlock: the dispatcher does not wake into a held lock
         const int frc = fill(s->in + r.off);
         lk.lock();
         if (--s->copying == 0) cv_disp_.notify_all();
@@ -514,6 +514,8 @@ class CoalescingQueue {
         std::vector<uint8_t>& rdy = early_[lane];
         rdy.assign(s.chunks.size(), 0);  // the slot is closed: its request list does not change
         size_t left = s.chunks.size();
+        std::vector<std::condition_variable*>& wake = wake_[lane];
+        wake.clear();
         for (;;) {
             bool fin = false;
             const int rc = b_.poll(s, rdy.data(), &fin);
@@ -526,11 +528,17 @@ class CoalescingQueue {
                     rdy[i] = 2;  // completed early: the request may be gone once its caller wakes
                     s.chunks[i]->status = 0;
                     s.chunks[i]->done = true;
-                    done_cv(s.chunks[i]).notify_all();  // lock held: the request is still there
+                    wake.push_back(&done_cv(s.chunks[i]));
                     early_done_++;
                     left--;
                 }
-            if (any) lk.unlock();
+            if (any) {
+                // notified after the unlock (the variables are the queue's, the requests may
+                // already be gone): a woken caller does not block again on the queue lock
+                lk.unlock();
+                for (auto* cv : wake) cv->notify_all();
+                wake.clear();
+            }
             if (left == 0) return b_.wait(s);  // nothing else can complete early
             std::this_thread::sleep_for(std::chrono::microseconds(c_.poll_us));
         }
@@ -572,12 +580,12 @@ class CoalescingQueue {
                 if (polled && early_[lane][i] == 2) continue;  // completed (and maybe gone) already
                 s->chunks[i]->status = s->status;
                 s->chunks[i]->done = true;
-                done_cv(s->chunks[i]).notify_all();
+                wake_[lane].push_back(&done_cv(s->chunks[i]));
             }
             for (QReq* q : s->hashes) {
                 q->status = s->status;
                 q->done = true;
-                done_cv(q).notify_all();
+                wake_[lane].push_back(&done_cv(q));
             }
             if (s->readers == 0) {  // every caller completed early and has left
                 s->state = QSlot::kFree;
@@ -586,6 +594,12 @@ class CoalescingQueue {
             cv_disp_.notify_all();
             if (disp_done_ && inflight_ == 0)
                 for (auto& cv : comp_cv_) cv.notify_all();
+            if (!wake_[lane].empty()) {  // the pass's remaining callers, woken outside the lock
+                lk.unlock();
+                for (auto* cv : wake_[lane]) cv->notify_all();
+                wake_[lane].clear();
+                lk.lock();
+            }
         }
     }
 
@@ -608,6 +622,7 @@ class CoalescingQueue {
     std::vector<std::condition_variable> comp_cv_;  // per lane
     std::vector<int> lane_busy_;
     std::vector<std::vector<uint8_t>> early_;  // per lane: its slot's requests completed early (2)
+    std::vector<std::vector<std::condition_variable*>> wake_;  // per lane: completions to notify
     std::thread disp_;
     std::vector<std::thread> comp_;
     int open_ = -1;
