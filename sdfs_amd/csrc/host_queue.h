@@ -319,7 +319,11 @@ class CoalescingQueue {
         cv_disp_.notify_one();  // after the unlock: the dispatcher does not wake into a held lock
         const int frc = fill(s->in + r.off);
         lk.lock();
-        if (--s->copying == 0) cv_disp_.notify_all();
+        if (--s->copying == 0) {  // the last copy: the dispatcher may launch (woken unlocked)
+            lk.unlock();
+            cv_disp_.notify_all();
+            lk.lock();
+        }
         done_cv(&r).wait(lk, [&] { return r.done; });  // woken with its own request (about) only
         lk.unlock();
         const int ret = frc ? frc : read(*s, r, r.status);
@@ -331,6 +335,7 @@ class CoalescingQueue {
             admit_waiting();
         }
         leave();
+        flush_admits(lk, false);
         return ret;
     }
 
@@ -428,8 +433,19 @@ class CoalescingQueue {
         return 1;
     }
 
+    // Wakes the callers admit_waiting placed, after releasing the queue lock (relock: take it
+    // again before returning).  Every admit_waiting() is followed by one of these.
+    void flush_admits(std::unique_lock<std::mutex>& lk, bool relock) {
+        if (admit_wake_.empty()) return;
+        std::vector<std::condition_variable*> adm;
+        adm.swap(admit_wake_);
+        lk.unlock();
+        for (auto* cv : adm) cv->notify_all();
+        if (relock) lk.lock();
+    }
+
     // Room may have appeared (a slot launched or freed): place waiting requests in arrival order
-    // while they fit and wake their callers (queue lock held).
+    // while they fit and mark their callers to wake (queue lock held; flush_admits wakes them).
     void admit_waiting() {
         if (stop_) return;  // the waiting callers see stop_ and leave
         bool any = false;
@@ -439,7 +455,7 @@ class CoalescingQueue {
             if (rc == 0) break;
             waitq_.pop_front();
             q->admit = rc;
-            admit_cv(q).notify_all();
+            admit_wake_.push_back(&admit_cv(q));  // notified by flush_admits, after the unlock
             any = true;
         }
         if (any) cv_disp_.notify_one();
@@ -491,6 +507,7 @@ class CoalescingQueue {
                 if (lane_busy_[l] < lane_busy_[lane]) lane = l;
             lane_busy_[lane]++;
             admit_waiting();  // waiting callers may open the next slot now
+            flush_admits(lk, true);
             cv_disp_.wait(lk, [&] { return s.copying == 0; });
             s.readers = (int)s.nreq();
             launched_++;
@@ -502,7 +519,9 @@ class CoalescingQueue {
             s.status = rc;
             s.state = QSlot::kFlight;
             flight_[lane].push_back(&s);
+            lk.unlock();
             comp_cv_[lane].notify_one();
+            lk.lock();
         }
         disp_done_ = true;  // completers may end once nothing is in flight
         for (auto& cv : comp_cv_) cv.notify_all();
@@ -594,9 +613,13 @@ class CoalescingQueue {
             cv_disp_.notify_all();
             if (disp_done_ && inflight_ == 0)
                 for (auto& cv : comp_cv_) cv.notify_all();
-            if (!wake_[lane].empty()) {  // the pass's remaining callers, woken outside the lock
+            if (!wake_[lane].empty() || !admit_wake_.empty()) {
+                // the pass's remaining callers and newly admitted ones, woken outside the lock
+                std::vector<std::condition_variable*> adm;
+                adm.swap(admit_wake_);
                 lk.unlock();
                 for (auto* cv : wake_[lane]) cv->notify_all();
+                for (auto* cv : adm) cv->notify_all();
                 wake_[lane].clear();
                 lk.lock();
             }
@@ -623,6 +646,7 @@ class CoalescingQueue {
     std::vector<int> lane_busy_;
     std::vector<std::vector<uint8_t>> early_;  // per lane: its slot's requests completed early (2)
     std::vector<std::vector<std::condition_variable*>> wake_;  // per lane: completions to notify
+    std::vector<std::condition_variable*> admit_wake_;  // admissions to notify (queue lock)
     std::thread disp_;
     std::vector<std::thread> comp_;
     int open_ = -1;
