@@ -287,8 +287,8 @@ struct DevEngine {
     bool split_packed = true;
     bool split_spread = false;  // one latency-form workgroup per CU for small passes (tuning: SDFS_SPLIT_SPREAD)
     bool split_masked = false;  // tuning: SDFS_SPLIT_MASKED (latency form, finished lanes masked off)
-    bool split_bybuf = false;   // latency-form groups per buffer, not per 32 longest (tuning: SDFS_SPLIT_BYBUF;
-                                // measured slower)
+    bool split_bybuf = true;    // latency-form groups per buffer, not per 32 longest (tuning: SDFS_SPLIT_BYBUF;
+                                // DESIGN.md §14)
     // small-batch cut walk: candidate list + successors (tuning: SDFS_SMALL_BALLOT=1 = ballots only)
     bool small_ballot = false;
     hipEvent_t ev_front = nullptr;
@@ -767,9 +767,9 @@ int run_pipeline(DevEngine* e, Workspace* w, const uint8_t* d_data, uint64_t dat
             // issue at a fraction of a lone wave's rate (tuning: SDFS_SPLIT_SPREAD)
             const uint64_t groups = (max_tasks + 31) / 32;
             const uint32_t pad = e->split_spread && groups <= (uint64_t)e->num_cus ? kSplitSpreadPad : 0u;
-            // groups drawn from one buffer would end that buffer with its own longest chunk
-            // instead of the group holding the pass's 32 longest — but they put more long chains
-            // side by side on the SIMDs, and measured slower at 1-128 callers
+            // groups drawn from one buffer end that buffer with its own longest chunk instead of
+            // the group holding the pass's 32 longest (every group of such a pass runs at once):
+            // 48 callers +16 % at the reference default, +4 % at the 4 KiB mix
             ha.split_masked = e->split_masked;
             if (e->split_bybuf && e->split_packed) {
                 ha.bybuf = (out->cap + 31) / 32;
