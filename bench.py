@@ -300,7 +300,7 @@ def threads_sweep(eng_cfg, device, host, buf_len, thread_counts, mode="fill"):
     T.getchunks(eng, tmax, host, buf_len, max(256, 4 * tmax), mode=mode)
     start = eng.queue_stats()
     for th in thread_counts:
-        calls = max(256, th * 8)
+        calls = max(512, th * 48)  # >= 48 calls per thread: a few ms per point is too noisy to compare
         r, _ = T.getchunks(eng, th, host, buf_len, calls, mode=mode)
         b0 = eng.queue_stats()
         out[str(th)] = {"gibps": round(r.gibps, 3), "p50_us": round(r.p50_us, 1), "p99_us": round(r.p99_us, 1),
